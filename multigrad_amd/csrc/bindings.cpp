@@ -1,0 +1,48 @@
+// Python bindings for the multigrad_amd native extension (_C).
+#include <torch/extension.h>
+
+#include <tuple>
+#include <vector>
+
+namespace mg {
+// smf.hip
+int smf_padded_bins(int64_t nb);
+void smf_forward(torch::Tensor x, c10::optional<torch::Tensor> pop, torch::Tensor theta,
+                 std::vector<double> edges, std::vector<double> scale, bool log_sigma,
+                 int64_t begin, int64_t end, torch::Tensor slab, int64_t nblocks);
+void smf_slab_reduce(torch::Tensor slab, int64_t nrows, std::vector<double> edges,
+                     std::vector<double> scale, torch::Tensor out);
+void smf_edge_weights(torch::Tensor g, std::vector<double> edges, std::vector<double> scale,
+                      torch::Tensor h);
+void smf_logmse(torch::Tensor S, torch::Tensor target, double eps, std::vector<double> edges,
+                std::vector<double> scale, torch::Tensor loss, torch::Tensor g_out,
+                torch::Tensor h);
+void smf_vjp(torch::Tensor x, c10::optional<torch::Tensor> pop, torch::Tensor theta,
+             torch::Tensor tiles, int64_t tile_begin, int64_t tile_end, torch::Tensor h,
+             std::vector<double> edges, std::vector<double> scale, bool log_sigma,
+             torch::Tensor grad, torch::Tensor partials, torch::Tensor giant);
+// adam.hip
+void fused_adam(torch::Tensor u, torch::Tensor m, torch::Tensor v, torch::Tensor g,
+                c10::optional<torch::Tensor> p, c10::optional<torch::Tensor> lo,
+                c10::optional<torch::Tensor> hi, c10::optional<torch::Tensor> kind,
+                torch::Tensor step, double lr, double b1, double b2, double eps, bool legacy,
+                c10::optional<torch::Tensor> traj, int64_t traj_stride);
+// runtime.cpp
+std::tuple<torch::Tensor, torch::Tensor, torch::Tensor, torch::Tensor, int64_t>
+build_tiles(torch::Tensor counts, std::vector<int64_t> breaks, int64_t tile_halos,
+            int64_t tile_pops);
+std::tuple<torch::Tensor, torch::Tensor> sort_by_population(torch::Tensor pop, int64_t npop);
+}  // namespace mg
+
+PYBIND11_MODULE(_C, m) {
+  m.doc() = "multigrad_amd native extension (gfx950 HIP kernels + host runtime)";
+  m.def("smf_padded_bins", &mg::smf_padded_bins);
+  m.def("smf_forward", &mg::smf_forward);
+  m.def("smf_slab_reduce", &mg::smf_slab_reduce);
+  m.def("smf_edge_weights", &mg::smf_edge_weights);
+  m.def("smf_logmse", &mg::smf_logmse);
+  m.def("smf_vjp", &mg::smf_vjp);
+  m.def("fused_adam", &mg::fused_adam);
+  m.def("build_tiles", &mg::build_tiles);
+  m.def("sort_by_population", &mg::sort_by_population);
+}

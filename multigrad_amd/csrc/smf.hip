@@ -1,0 +1,470 @@
+// Stellar-mass-function (SMF) summed-statistic kernels for gfx950 (MI355X).
+//
+// Model (reference tests/smf_example/smf_grad_descent.py:32-48 and
+// docs/source/notebooks/smf_gradient_descent.py:20-35, generalised to populations):
+//   halo i belongs to population c_i; theta is interleaved (a_c, s_c) per population;
+//   mu_i = x_i + a_c ;  sigma_c = LOGSIG ? 10^{s_c} : s_c
+//   S_k  = scale_k * sum_i [ Phi((e_{k+1}-mu_i)/sigma) - Phi((e_k-mu_i)/sigma) ]
+// The reference issues one XLA dispatch per bin with 2 erf per halo per bin; here ONE
+// pass evaluates all NB+1 edge tails per halo (tail-accurate Q(z), see common.h), keeps
+// the NB bin sums in registers across a grid-stride loop, and reduces them
+// deterministically (wave shuffles -> LDS -> per-block slab -> fixed-order slab sum).
+//
+// The VJP recomputes z (no O(N*K) residuals) and contracts the edge
+// weights h_e = (g_{e-1} scale_{e-1} - g_e scale_e)/sqrt(2 pi) with the Gaussian pdf in
+// registers.  Per-population gradients are a *segmented* reduction over halos sorted
+// by population.  A host-built tile schedule (build_tiles) cuts the halo array at
+// population boundaries into tiles of <= 2048 halos / <= 2048 populations, so each tile
+// is owned by one workgroup: blocked per-thread segments + a block-wide segmented scan
+// write every population exactly once through LDS -- no float atomics, bitwise
+// reproducible.  Populations larger than a tile are split into "partial" tiles whose
+// sums are combined in a fixed order by a finalize kernel (this is also the path of the
+// 2-parameter shared-parameter models).
+#include "common.h"
+
+#include <torch/extension.h>
+#include <ATen/hip/HIPContext.h>
+#include <vector>
+
+namespace mg {
+
+constexpr int kMaxBins = 32;
+constexpr int kThreads = 256;
+constexpr int kItems = 8;                       // halos per thread in a tile
+constexpr int kTileHalos = kThreads * kItems;   // 2048
+constexpr int kTilePops = 2048;
+constexpr float kLn10 = 2.302585092994046f;
+constexpr float kLog2_10 = 3.321928094887362f;
+
+struct SmfBins {
+  float edge[kMaxBins + 1];  // NBP+1 edges (padded bins are zero width, scale 0)
+  float scale[kMaxBins];     // 1 / (volume * width) per bin
+};
+
+struct Tile {
+  int64_t h0, h1;  // halo range [h0, h1)
+  int32_t p0, p1;  // population range [p0, p1) (p1 = p0+1 for partial tiles)
+  int32_t slot;    // -1: whole populations; >=0: partial-sum slot of population p0
+  int32_t pad;
+};
+
+template <bool LOGSIG>
+__device__ __forceinline__ float inv_sigma(float s) {
+  return LOGSIG ? fast_exp2(-s * kLog2_10) : 1.0f / s;
+}
+
+// Accumulate the NB bin masses of one halo.
+template <int NB, bool LOGSIG>
+__device__ __forceinline__ void halo_mass(float x, float2 th, const SmfBins& b, float (&acc)[NB]) {
+  const float inv = inv_sigma<LOGSIG>(th.y);
+  const float nmi = -(x + th.x) * inv;  // -mu/sigma
+  float zp = fmaf(b.edge[0], inv, nmi);
+  float tp = normal_tail(zp);
+#pragma unroll
+  for (int k = 0; k < NB; ++k) {
+    const float z = fmaf(b.edge[k + 1], inv, nmi);
+    const float t = normal_tail(z);
+    // mass of (zp, z]: both tails on the same side -> difference of tails (no
+    // cancellation); straddling the mean -> 1 - both tails.
+    const float m = zp >= 0.0f ? tp - t : (z <= 0.0f ? t - tp : (1.0f - tp) - t);
+    acc[k] += m;
+    zp = z;
+    tp = t;
+  }
+}
+
+template <int NB, bool LOGSIG, bool HAS_POP>
+__global__ __launch_bounds__(kThreads) void smf_fwd_kernel(
+    const float* __restrict__ x, const int32_t* __restrict__ pop,
+    const float2* __restrict__ theta, int64_t begin, int64_t end, SmfBins bins,
+    float* __restrict__ slab) {
+  float acc[NB];
+#pragma unroll
+  for (int k = 0; k < NB; ++k) acc[k] = 0.0f;
+  const float2 th0 = HAS_POP ? make_float2(0.f, 0.f) : theta[0];
+  const int64_t stride = (int64_t)gridDim.x * kThreads;
+  for (int64_t i = begin + (int64_t)blockIdx.x * kThreads + threadIdx.x; i < end; i += stride) {
+    const float xi = x[i];
+    const float2 th = HAS_POP ? theta[pop[i]] : th0;
+    halo_mass<NB, LOGSIG>(xi, th, bins, acc);
+  }
+  __shared__ float scratch[NB * (kThreads / kWave)];
+  block_sum_n<NB>(acc, scratch);
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int k = 0; k < NB; ++k) slab[(int64_t)blockIdx.x * NB + k] = acc[k];
+  }
+}
+
+// Sum nrows slab rows per bin in a fixed order (double accumulation), apply the bin
+// scale, write (or add into) out[NB].
+__global__ __launch_bounds__(kThreads) void slab_reduce_kernel(
+    const float* __restrict__ slab, int nrows, int nb, SmfBins bins, float* __restrict__ out) {
+  __shared__ double scratch[kThreads / kWave];
+  for (int k = 0; k < nb; ++k) {
+    double s = 0.0;
+    for (int r = threadIdx.x; r < nrows; r += kThreads) s += (double)slab[(int64_t)r * nb + k];
+    double v[1] = {s};
+    block_sum_n<1>(v, scratch);
+    if (threadIdx.x == 0) out[k] = (float)(v[0] * (double)bins.scale[k]);
+    __syncthreads();
+  }
+}
+
+// Edge weights h_e from the sumstat cotangent g (dL/dS), folded with 1/sqrt(2 pi).
+__device__ __forceinline__ float edge_weight(const float* g, const SmfBins& b, int e, int nb) {
+  float h = 0.0f;
+  if (e >= 1) h += g[e - 1] * b.scale[e - 1];
+  if (e < nb) h -= g[e] * b.scale[e];
+  return h * 0.3989422804014327f;
+}
+
+__global__ void edge_weights_kernel(const float* __restrict__ g, int nb, SmfBins bins,
+                                    float* __restrict__ h) {
+  const int e = threadIdx.x;
+  if (e <= nb) h[e] = edge_weight(g, bins, e, nb);
+}
+
+// log-MSE loss on total sumstats (reference tests/smf_example/smf_grad_descent.py:78-82,
+// docs variant adds eps=1e-10): loss = mean_k (log10(S_k+eps) - log10(T_k+eps))^2.
+// Writes loss[0], the cotangent-derived edge weights h[0..nb] and dL/dS into g_out.
+__global__ void logmse_loss_kernel(const float* __restrict__ S, const float* __restrict__ target,
+                                   float eps, int nb, SmfBins bins, float* __restrict__ loss,
+                                   float* __restrict__ g_out, float* __restrict__ h) {
+  __shared__ float g[kMaxBins];
+  __shared__ float d2[kMaxBins];
+  const int k = threadIdx.x;
+  if (k < nb) {
+    const float s = S[k] + eps;
+    const float d = log10f(s) - log10f(target[k] + eps);
+    d2[k] = d * d;
+    g[k] = 2.0f / nb * d / (s * kLn10);
+    if (g_out) g_out[k] = g[k];
+  }
+  __syncthreads();
+  if (k == 0) {
+    float acc = 0.0f;
+    for (int j = 0; j < nb; ++j) acc += d2[j];
+    loss[0] = acc / nb;
+  }
+  if (k <= nb && h) h[k] = edge_weight(g, bins, k, nb);
+}
+
+template <int NB, bool LOGSIG>
+__device__ __forceinline__ void halo_vjp(float x, float2 th, float inv, const float (&h)[NB + 1],
+                                         const SmfBins& b, float& A, float& B) {
+  const float nmi = -(x + th.x) * inv;
+#pragma unroll
+  for (int e = 0; e <= NB; ++e) {
+    const float z = fmaf(b.edge[e], inv, nmi);
+    const float w = h[e] * fast_exp2(z * z * -0.72134752044448170f);
+    A += w;
+    B = fmaf(w, z, B);
+  }
+}
+
+template <bool LOGSIG>
+__device__ __forceinline__ float2 pop_grad(float2 th, float A, float B) {
+  const float inv = inv_sigma<LOGSIG>(th.y);
+  return make_float2(-inv * A, LOGSIG ? -kLn10 * B : -inv * B);
+}
+
+// Segmented-scan combine: (flag, A, B) pairs.
+struct Seg {
+  int f;
+  float a, b;
+};
+
+template <int NB, bool LOGSIG>
+__global__ __launch_bounds__(kThreads) void smf_vjp_tiles_kernel(
+    const float* __restrict__ x, const int32_t* __restrict__ pop,
+    const float2* __restrict__ theta, const Tile* __restrict__ tiles,
+    const float* __restrict__ hvec, SmfBins bins, float2* __restrict__ grad,
+    float2* __restrict__ partials) {
+  const Tile t = tiles[blockIdx.x];
+  float h[NB + 1];
+#pragma unroll
+  for (int e = 0; e <= NB; ++e) h[e] = hvec[e];
+  const int tid = threadIdx.x;
+  const int lane = tid & (kWave - 1);
+  const int wid = tid >> 6;
+
+  if (t.slot >= 0) {  // partial tile: one population, plain block reduction
+    const float2 th = theta[t.p0];
+    const float inv = inv_sigma<LOGSIG>(th.y);
+    float v[2] = {0.0f, 0.0f};
+    for (int64_t i = t.h0 + tid; i < t.h1; i += kThreads) halo_vjp<NB, LOGSIG>(x[i], th, inv, h, bins, v[0], v[1]);
+    __shared__ float scratch[2 * (kThreads / kWave)];
+    block_sum_n<2>(v, scratch);
+    if (tid == 0) partials[t.slot] = make_float2(v[0], v[1]);
+    return;
+  }
+
+  __shared__ float2 res[kTilePops];
+  __shared__ int s_tailpop[kThreads];
+  __shared__ int s_headpop[kThreads];
+  __shared__ float2 s_incl[kThreads];
+  __shared__ Seg s_wagg[kThreads / kWave];
+
+  const int npops = t.p1 - t.p0;
+  for (int k = tid; k < npops; k += kThreads) res[k] = make_float2(0.f, 0.f);
+
+  // ---- blocked per-thread sequential segmented reduction over <= kItems halos
+  const int64_t base = t.h0 + (int64_t)tid * kItems;
+  const int cnt = (int)max((int64_t)0, min((int64_t)kItems, t.h1 - base));
+  int headpop = -1, curpop = -1, nseg = 0;
+  float headA = 0.f, headB = 0.f, curA = 0.f, curB = 0.f;
+  float2 th = make_float2(0.f, 1.f);
+  float inv = 1.0f;
+  __syncthreads();  // res zeroed before any interior write
+  for (int j = 0; j < cnt; ++j) {
+    const int64_t i = base + j;
+    const int c = pop[i];
+    if (c != curpop) {
+      if (nseg == 1) {
+        headpop = curpop; headA = curA; headB = curB;
+      } else if (nseg > 1) {
+        // complete interior segment owned by this thread
+        res[curpop - t.p0] = make_float2(curA, curB);
+      }
+      curpop = c; curA = 0.f; curB = 0.f; ++nseg;
+      th = theta[c];
+      inv = inv_sigma<LOGSIG>(th.y);
+    }
+    halo_vjp<NB, LOGSIG>(x[i], th, inv, h, bins, curA, curB);
+  }
+  if (nseg == 1) { headpop = curpop; headA = curA; headB = curB; }
+  const bool boundary = nseg > 1;
+  // ---- block-wide segmented inclusive scan of the tail segments
+  s_headpop[tid] = cnt ? headpop : -1;
+  s_tailpop[tid] = cnt ? curpop : -1;
+  __syncthreads();
+  const int prevtail = tid ? s_tailpop[tid - 1] : -1;
+  Seg s;
+  s.f = (cnt == 0) || boundary || tid == 0 || prevtail != curpop;
+  s.a = cnt ? curA : 0.f;
+  s.b = cnt ? curB : 0.f;
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) {
+    const int f2 = __shfl_up(s.f, o, kWave);
+    const float a2 = __shfl_up(s.a, o, kWave);
+    const float b2 = __shfl_up(s.b, o, kWave);
+    if (lane >= o && !s.f) { s.a += a2; s.b += b2; }
+    if (lane >= o) s.f |= f2;
+  }
+  if (lane == kWave - 1) s_wagg[wid] = s;
+  __syncthreads();
+  if (!s.f) {  // no segment start between wave start and this lane: add earlier waves
+    for (int w = wid - 1; w >= 0; --w) {
+      const Seg g = s_wagg[w];
+      s.a += g.a; s.b += g.b;
+      if (g.f) break;
+    }
+  }
+  s_incl[tid] = make_float2(s.a, s.b);
+  __syncthreads();
+  // head segment completes inside this thread: add the carry from earlier threads
+  if (cnt && boundary) {
+    float2 carry = make_float2(0.f, 0.f);
+    if (tid && prevtail == headpop) carry = s_incl[tid - 1];
+    res[headpop - t.p0] = make_float2(headA + carry.x, headB + carry.y);
+  }
+  // tail segment ends here unless the next thread continues it
+  if (cnt) {
+    const int nexthead = tid + 1 < kThreads ? s_headpop[tid + 1] : -1;
+    if (nexthead != curpop) res[curpop - t.p0] = s_incl[tid];
+  }
+  __syncthreads();
+  for (int k = tid; k < npops; k += kThreads) {
+    const int c = t.p0 + k;
+    const float2 r = res[k];
+    grad[c] = pop_grad<LOGSIG>(theta[c], r.x, r.y);
+  }
+}
+
+// giant[g] = {pop, slot_begin, slot_end}: sum partial slots in order.
+template <bool LOGSIG>
+__global__ __launch_bounds__(kThreads) void smf_vjp_finalize_kernel(
+    const int32_t* __restrict__ giant, const float2* __restrict__ partials,
+    const float2* __restrict__ theta, float2* __restrict__ grad) {
+  const int c = giant[3 * blockIdx.x], s0 = giant[3 * blockIdx.x + 1], s1 = giant[3 * blockIdx.x + 2];
+  double v[2] = {0.0, 0.0};
+  for (int s = s0 + threadIdx.x; s < s1; s += kThreads) {
+    const float2 p = partials[s];
+    v[0] += p.x; v[1] += p.y;
+  }
+  __shared__ double scratch[2 * (kThreads / kWave)];
+  block_sum_n<2>(v, scratch);
+  if (threadIdx.x == 0) grad[c] = pop_grad<LOGSIG>(theta[c], (float)v[0], (float)v[1]);
+}
+
+// ------------------------------------------------------------------ host side
+static int padded_bins(int nb) {
+  const int sizes[] = {1, 2, 4, 8, 10, 16, 32};
+  for (int s : sizes)
+    if (nb <= s) return s;
+  TORCH_CHECK(false, "at most ", kMaxBins, " bins supported, got ", nb);
+  return 0;
+}
+
+static SmfBins make_bins(const std::vector<double>& edges, const std::vector<double>& scale, int nbp) {
+  const int nb = (int)scale.size();
+  TORCH_CHECK((int)edges.size() == nb + 1, "need nb+1 edges");
+  SmfBins b;
+  for (int e = 0; e <= kMaxBins; ++e) b.edge[e] = (float)edges[std::min(e, nb)];
+  for (int k = 0; k < kMaxBins; ++k) b.scale[k] = k < nb ? (float)scale[k] : 0.0f;
+  (void)nbp;
+  return b;
+}
+
+#define MG_DISPATCH_NB(NBP, ...)                             \
+  switch (NBP) {                                             \
+    case 1: { constexpr int NB = 1; __VA_ARGS__; break; }    \
+    case 2: { constexpr int NB = 2; __VA_ARGS__; break; }    \
+    case 4: { constexpr int NB = 4; __VA_ARGS__; break; }    \
+    case 8: { constexpr int NB = 8; __VA_ARGS__; break; }    \
+    case 10: { constexpr int NB = 10; __VA_ARGS__; break; }  \
+    case 16: { constexpr int NB = 16; __VA_ARGS__; break; }  \
+    default: { constexpr int NB = 32; __VA_ARGS__; break; }  \
+  }
+
+static void check_dev(const torch::Tensor& t, const char* name, at::ScalarType st) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a device tensor");
+  TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
+  TORCH_CHECK(t.scalar_type() == st, name, " has wrong dtype");
+}
+
+int smf_padded_bins(int64_t nb) { return padded_bins((int)nb); }
+
+// Forward over halos [begin, end); writes slab[nblocks * NBP].
+void smf_forward(torch::Tensor x, c10::optional<torch::Tensor> pop, torch::Tensor theta,
+                 std::vector<double> edges, std::vector<double> scale, bool log_sigma,
+                 int64_t begin, int64_t end, torch::Tensor slab, int64_t nblocks) {
+  check_dev(x, "x", at::kFloat);
+  check_dev(theta, "theta", at::kFloat);
+  check_dev(slab, "slab", at::kFloat);
+  const int nbp = padded_bins((int)scale.size());
+  TORCH_CHECK(begin >= 0 && end <= x.numel() && begin <= end, "bad halo range");
+  TORCH_CHECK(slab.numel() >= nblocks * nbp, "slab too small");
+  TORCH_CHECK(nblocks >= 1 && nblocks <= 65535, "bad block count");
+  const bool has_pop = pop.has_value() && pop->defined();
+  if (has_pop) {
+    check_dev(*pop, "pop", at::kInt);
+    TORCH_CHECK(pop->numel() == x.numel(), "pop/x size mismatch");
+  } else {
+    TORCH_CHECK(theta.numel() >= 2, "theta needs 2 entries");
+  }
+  const SmfBins b = make_bins(edges, scale, nbp);
+  auto stream = at::hip::getCurrentHIPStream();
+  const float* xp = x.data_ptr<float>();
+  const int32_t* pp = has_pop ? pop->data_ptr<int32_t>() : nullptr;
+  const float2* tp = reinterpret_cast<const float2*>(theta.data_ptr<float>());
+  float* sp = slab.data_ptr<float>();
+  MG_DISPATCH_NB(nbp, {
+    if (log_sigma) {
+      if (has_pop) hipLaunchKernelGGL((smf_fwd_kernel<NB, true, true>), dim3(nblocks), dim3(kThreads), 0, stream, xp, pp, tp, begin, end, b, sp);
+      else hipLaunchKernelGGL((smf_fwd_kernel<NB, true, false>), dim3(nblocks), dim3(kThreads), 0, stream, xp, pp, tp, begin, end, b, sp);
+    } else {
+      if (has_pop) hipLaunchKernelGGL((smf_fwd_kernel<NB, false, true>), dim3(nblocks), dim3(kThreads), 0, stream, xp, pp, tp, begin, end, b, sp);
+      else hipLaunchKernelGGL((smf_fwd_kernel<NB, false, false>), dim3(nblocks), dim3(kThreads), 0, stream, xp, pp, tp, begin, end, b, sp);
+    }
+  });
+}
+
+void smf_slab_reduce(torch::Tensor slab, int64_t nrows, std::vector<double> edges,
+                     std::vector<double> scale, torch::Tensor out) {
+  check_dev(slab, "slab", at::kFloat);
+  check_dev(out, "out", at::kFloat);
+  const int nbp = padded_bins((int)scale.size());
+  TORCH_CHECK(slab.numel() >= nrows * nbp, "slab too small");
+  TORCH_CHECK(out.numel() >= nbp, "out too small");
+  const SmfBins b = make_bins(edges, scale, nbp);
+  auto stream = at::hip::getCurrentHIPStream();
+  hipLaunchKernelGGL(slab_reduce_kernel, dim3(1), dim3(kThreads), 0, stream,
+                     slab.data_ptr<float>(), (int)nrows, nbp, b, out.data_ptr<float>());
+}
+
+void smf_edge_weights(torch::Tensor g, std::vector<double> edges, std::vector<double> scale,
+                      torch::Tensor h) {
+  check_dev(g, "g", at::kFloat);
+  check_dev(h, "h", at::kFloat);
+  const int nb = (int)scale.size();
+  const int nbp = padded_bins(nb);
+  TORCH_CHECK(g.numel() >= nb && h.numel() >= nbp + 1, "bad sizes");
+  const SmfBins b = make_bins(edges, scale, nbp);
+  auto stream = at::hip::getCurrentHIPStream();
+  // padded edges (e > nb) must get weight 0: zero h first
+  hipMemsetAsync(h.data_ptr<float>(), 0, sizeof(float) * (nbp + 1), stream);
+  hipLaunchKernelGGL(edge_weights_kernel, dim3(1), dim3(64), 0, stream, g.data_ptr<float>(), nb,
+                     b, h.data_ptr<float>());
+}
+
+void smf_logmse(torch::Tensor S, torch::Tensor target, double eps, std::vector<double> edges,
+                std::vector<double> scale, torch::Tensor loss, torch::Tensor g_out,
+                torch::Tensor h) {
+  check_dev(S, "S", at::kFloat);
+  check_dev(target, "target", at::kFloat);
+  check_dev(loss, "loss", at::kFloat);
+  check_dev(h, "h", at::kFloat);
+  const int nb = (int)scale.size();
+  const int nbp = padded_bins(nb);
+  TORCH_CHECK(S.numel() >= nb && target.numel() >= nb && h.numel() >= nbp + 1, "bad sizes");
+  const SmfBins b = make_bins(edges, scale, nbp);
+  auto stream = at::hip::getCurrentHIPStream();
+  float* gp = nullptr;
+  if (g_out.defined() && g_out.numel()) {
+    check_dev(g_out, "g_out", at::kFloat);
+    gp = g_out.data_ptr<float>();
+  }
+  if (nbp > nb) hipMemsetAsync(h.data_ptr<float>(), 0, sizeof(float) * (nbp + 1), stream);
+  hipLaunchKernelGGL(logmse_loss_kernel, dim3(1), dim3(64), 0, stream, S.data_ptr<float>(),
+                     target.data_ptr<float>(), (float)eps, nb, b, loss.data_ptr<float>(), gp,
+                     h.data_ptr<float>());
+}
+
+// VJP over a tile schedule; grad is interleaved [2 * npop]; partials [nslots * 2].
+void smf_vjp(torch::Tensor x, c10::optional<torch::Tensor> pop, torch::Tensor theta,
+             torch::Tensor tiles, int64_t tile_begin, int64_t tile_end, torch::Tensor h,
+             std::vector<double> edges, std::vector<double> scale, bool log_sigma,
+             torch::Tensor grad, torch::Tensor partials, torch::Tensor giant) {
+  check_dev(x, "x", at::kFloat);
+  check_dev(theta, "theta", at::kFloat);
+  check_dev(h, "h", at::kFloat);
+  check_dev(grad, "grad", at::kFloat);
+  check_dev(tiles, "tiles", at::kLong);
+  TORCH_CHECK(tiles.size(1) == 4, "tiles must be [ntiles, 4] int64 (32-byte records)");
+  const int nbp = padded_bins((int)scale.size());
+  TORCH_CHECK(h.numel() >= nbp + 1, "h too small");
+  TORCH_CHECK(grad.numel() == theta.numel(), "grad/theta size mismatch");
+  const bool has_pop = pop.has_value() && pop->defined();
+  if (has_pop) check_dev(*pop, "pop", at::kInt);
+  const int64_t ntiles = tile_end - tile_begin;
+  TORCH_CHECK(tile_begin >= 0 && tile_end <= tiles.size(0) && ntiles >= 0, "bad tile range");
+  const SmfBins b = make_bins(edges, scale, nbp);
+  auto stream = at::hip::getCurrentHIPStream();
+  const float* xp = x.data_ptr<float>();
+  const int32_t* pp = has_pop ? pop->data_ptr<int32_t>() : nullptr;
+  const float2* tp = reinterpret_cast<const float2*>(theta.data_ptr<float>());
+  const Tile* tl = reinterpret_cast<const Tile*>(tiles.data_ptr<int64_t>()) + tile_begin;
+  float2* gp = reinterpret_cast<float2*>(grad.data_ptr<float>());
+  float2* pa = partials.numel() ? reinterpret_cast<float2*>(partials.data_ptr<float>()) : nullptr;
+  if (ntiles > 0) {
+    MG_DISPATCH_NB(nbp, {
+      if (log_sigma)
+        hipLaunchKernelGGL((smf_vjp_tiles_kernel<NB, true>), dim3(ntiles), dim3(kThreads), 0, stream, xp, pp, tp, tl, h.data_ptr<float>(), b, gp, pa);
+      else
+        hipLaunchKernelGGL((smf_vjp_tiles_kernel<NB, false>), dim3(ntiles), dim3(kThreads), 0, stream, xp, pp, tp, tl, h.data_ptr<float>(), b, gp, pa);
+    });
+  }
+  const int64_t ng = giant.numel() / 3;
+  if (ng > 0) {
+    check_dev(giant, "giant", at::kInt);
+    TORCH_CHECK(pa != nullptr, "partials buffer required");
+    if (log_sigma)
+      hipLaunchKernelGGL((smf_vjp_finalize_kernel<true>), dim3(ng), dim3(kThreads), 0, stream, giant.data_ptr<int32_t>(), pa, tp, gp);
+    else
+      hipLaunchKernelGGL((smf_vjp_finalize_kernel<false>), dim3(ng), dim3(kThreads), 0, stream, giant.data_ptr<int32_t>(), pa, tp, gp);
+  }
+}
+
+}  // namespace mg

@@ -1,0 +1,222 @@
+"""SMF summed-statistic ops: HIP forward/VJP kernels + fp32/fp64 PyTorch references.
+
+Device tensors run ``csrc/smf.hip`` (one pass over the halos for all bins, deterministic
+reductions, segmented per-population VJP).  CPU tensors use the PyTorch formulation
+below, which is also the numerics oracle for the kernel tests.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+from typing import List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from ._ext import ext
+
+__all__ = ["SmfBins", "PopulationShard", "smf_sumstats", "smf_sumstats_reference",
+           "logmse_loss", "normal_cdf", "TILE_HALOS", "TILE_POPS"]
+
+TILE_HALOS = 2048
+TILE_POPS = 2048
+FWD_BLOCKS_MAX = 2048  # 8 workgroups per CU on 256 CUs, grid-stride beyond
+
+
+@dataclass(frozen=True)
+class SmfBins:
+    """Bin edges and per-bin scale ``1/(volume*width)`` of a stellar-mass function."""
+
+    edges: tuple
+    scale: tuple
+
+    @staticmethod
+    def make(edges, volume: float) -> "SmfBins":
+        e = np.asarray(torch.as_tensor(edges).detach().cpu().double().numpy() if
+                       isinstance(edges, torch.Tensor) else edges, dtype=np.float64)
+        w = np.diff(e)
+        return SmfBins(tuple(float(v) for v in e), tuple(float(1.0 / (volume * d)) for d in w))
+
+    @property
+    def nb(self) -> int:
+        return len(self.scale)
+
+    @property
+    def nbp(self) -> int:
+        for s in (1, 2, 4, 8, 10, 16, 32):
+            if self.nb <= s:
+                return s
+        raise ValueError("at most 32 bins supported by the HIP kernels")
+
+
+def normal_cdf(z: torch.Tensor) -> torch.Tensor:
+    return torch.special.ndtr(z)
+
+
+def smf_sumstats_reference(theta: torch.Tensor, x: torch.Tensor, pop: Optional[torch.Tensor],
+                           bins: SmfBins, log_sigma: bool) -> torch.Tensor:
+    """Differentiable PyTorch SMF (any dtype/device): S_k = scale_k sum_i dPhi_ik."""
+    th = theta.reshape(-1, 2)
+    a = th[:, 0]
+    s = th[:, 1]
+    if pop is None:
+        a_i, s_i = a[0], s[0]
+    else:
+        idx = pop.long()
+        a_i, s_i = a[idx], s[idx]
+    sigma = torch.pow(torch.as_tensor(10.0, dtype=theta.dtype, device=theta.device), s_i) \
+        if log_sigma else s_i
+    mu = x.to(theta.dtype) + a_i
+    edges = torch.as_tensor(bins.edges, dtype=theta.dtype, device=theta.device)
+    scale = torch.as_tensor(bins.scale, dtype=theta.dtype, device=theta.device)
+    if sigma.dim() == 0:
+        z = (edges[None, :] - mu[:, None]) / sigma
+    else:
+        z = (edges[None, :] - mu[:, None]) / sigma[:, None]
+    cdf = normal_cdf(z)
+    mass = (cdf[:, 1:] - cdf[:, :-1]).sum(0)
+    return mass * scale
+
+
+def logmse_loss(sumstats: torch.Tensor, target: torch.Tensor, eps: float = 0.0) -> torch.Tensor:
+    """Reduced chi^2 with unit errors in log10 space (reference smf_grad_descent.py:78-82)."""
+    return torch.mean((torch.log10(sumstats + eps) - torch.log10(target + eps)) ** 2)
+
+
+class PopulationShard:
+    """This rank's data shard sorted by population, with the device tile schedule.
+
+    Parameters
+    ----------
+    x : (N,) float tensor of log halo masses (any order)
+    pop : (N,) int tensor of population ids in ``[0, npop)``, or None for a single
+        shared-parameter population (the reference's 2-parameter models)
+    npop : number of populations (parameters = 2 * npop)
+    device : device for the kernels
+    chunks : number of contiguous population chunks (tiles never straddle a chunk, so
+        per-chunk VJPs can overlap per-chunk gradient collectives)
+    """
+
+    def __init__(self, x, pop=None, npop: int = 1, device=None, chunks: int = 1,
+                 tile_halos: int = TILE_HALOS, tile_pops: int = TILE_POPS):
+        x = torch.as_tensor(x)
+        device = torch.device(device) if device is not None else x.device
+        self.device = device
+        self.npop = int(npop)
+        self.n = int(x.numel())
+        if pop is None:
+            assert self.npop == 1
+            xs = x.reshape(-1).to(device=device, dtype=torch.float32).contiguous()
+            counts = torch.tensor([self.n], dtype=torch.int64)
+            self.pop = None
+        else:
+            pop_cpu = torch.as_tensor(pop).reshape(-1).to("cpu", torch.int32).contiguous()
+            order, counts = _sort_by_population(pop_cpu, self.npop)
+            xs = x.reshape(-1)[order.to(x.device)].to(device=device, dtype=torch.float32).contiguous()
+            self.pop = pop_cpu[order].to(device).contiguous()
+        self.x = xs
+        self.counts = counts
+        self.offsets = torch.zeros(self.npop + 1, dtype=torch.int64)
+        self.offsets[1:] = torch.cumsum(counts, 0)
+        self.nchunks = max(1, min(int(chunks), self.npop))
+        bounds = np.linspace(0, self.npop, self.nchunks + 1).round().astype(np.int64)
+        self.chunk_pops = [int(b) for b in bounds]
+        self.chunk_halos = [int(self.offsets[b]) for b in bounds]
+        tiles, giant, ct, cg, nslots = _build_tiles(counts, self.chunk_pops[1:-1], tile_halos, tile_pops)
+        self.tiles = tiles.to(device)
+        self.giant = giant.to(device)
+        self.chunk_tiles = [int(v) for v in ct]
+        self.chunk_giant = [int(v) for v in cg]
+        self.nslots = int(nslots)
+        self.partials = torch.zeros(max(self.nslots, 1) * 2, dtype=torch.float32, device=device)
+
+    def fwd_blocks(self, nhalos: int) -> int:
+        return int(max(1, min(FWD_BLOCKS_MAX, math.ceil(nhalos / 256))))
+
+
+def _sort_by_population(pop_cpu: torch.Tensor, npop: int):
+    try:
+        return ext().sort_by_population(pop_cpu, npop)
+    except ImportError:
+        order = torch.argsort(pop_cpu.long(), stable=True)
+        counts = torch.bincount(pop_cpu.long(), minlength=npop)
+        return order, counts
+
+
+def _build_tiles(counts, breaks, tile_halos, tile_pops):
+    try:
+        return ext().build_tiles(counts.to(torch.int64), list(breaks), tile_halos, tile_pops)
+    except ImportError:
+        from ._schedule import build_tiles_py
+        return build_tiles_py(counts, breaks, tile_halos, tile_pops)
+
+
+# ---------------------------------------------------------------------------- device ops
+def smf_forward_into(theta: torch.Tensor, shard: PopulationShard, bins: SmfBins, log_sigma: bool,
+                     out: torch.Tensor, slab: Optional[torch.Tensor] = None,
+                     chunk: Optional[int] = None) -> torch.Tensor:
+    """Partial sumstats of the shard (or one population chunk) into ``out[:nbp]``."""
+    E = ext()
+    if chunk is None:
+        h0, h1 = 0, shard.n
+    else:
+        h0, h1 = shard.chunk_halos[chunk], shard.chunk_halos[chunk + 1]
+    nblk = shard.fwd_blocks(max(h1 - h0, 1))
+    if slab is None:
+        slab = torch.empty(nblk * bins.nbp, dtype=torch.float32, device=theta.device)
+    E.smf_forward(shard.x, shard.pop, theta, list(bins.edges), list(bins.scale), bool(log_sigma),
+                  h0, h1, slab, nblk)
+    E.smf_slab_reduce(slab, nblk, list(bins.edges), list(bins.scale), out)
+    return out
+
+
+def smf_vjp_into(theta: torch.Tensor, shard: PopulationShard, bins: SmfBins, log_sigma: bool,
+                 h: torch.Tensor, grad: torch.Tensor, chunk: Optional[int] = None) -> torch.Tensor:
+    E = ext()
+    if chunk is None:
+        t0, t1 = 0, shard.tiles.shape[0]
+        g0, g1 = 0, shard.giant.shape[0]
+    else:
+        t0, t1 = shard.chunk_tiles[chunk], shard.chunk_tiles[chunk + 1]
+        g0, g1 = shard.chunk_giant[chunk], shard.chunk_giant[chunk + 1]
+    E.smf_vjp(shard.x, shard.pop, theta, shard.tiles, t0, t1, h, list(bins.edges),
+              list(bins.scale), bool(log_sigma), grad, shard.partials, shard.giant[g0:g1])
+    return grad
+
+
+class _SmfSumstats(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, theta, shard, bins, log_sigma):
+        out = torch.empty(bins.nbp, dtype=torch.float32, device=theta.device)
+        smf_forward_into(theta.detach().contiguous(), shard, bins, log_sigma, out)
+        ctx.shard, ctx.bins, ctx.log_sigma = shard, bins, log_sigma
+        ctx.save_for_backward(theta)
+        return out[:bins.nb].clone()
+
+    @staticmethod
+    def backward(ctx, gS):
+        (theta,) = ctx.saved_tensors
+        bins = ctx.bins
+        g = gS.detach().to(torch.float32).contiguous()
+        h = torch.empty(bins.nbp + 1, dtype=torch.float32, device=theta.device)
+        ext().smf_edge_weights(g, list(bins.edges), list(bins.scale), h)
+        grad = torch.empty_like(theta, dtype=torch.float32)
+        smf_vjp_into(theta.detach().contiguous(), ctx.shard, bins, ctx.log_sigma, h, grad)
+        return grad.to(theta.dtype), None, None, None
+
+
+def smf_sumstats(theta: torch.Tensor, shard: PopulationShard, bins: SmfBins,
+                 log_sigma: bool = True) -> torch.Tensor:
+    """Partial SMF of this rank's shard; differentiable w.r.t. interleaved ``theta``.
+
+    ``theta`` holds ``(a_c, s_c)`` per population (``2 * npop`` values).  On a GPU this
+    runs the HIP kernels (float32); on CPU the PyTorch reference.
+    """
+    if theta.device.type == "cuda":
+        th = theta.reshape(-1)
+        if th.dtype != torch.float32:
+            th = th.to(torch.float32)
+        return _SmfSumstats.apply(th, shard, bins, bool(log_sigma)).to(theta.dtype)
+    return smf_sumstats_reference(theta.reshape(-1), shard.x.to(theta.device),
+                                  None if shard.pop is None else shard.pop.to(theta.device),
+                                  bins, log_sigma)

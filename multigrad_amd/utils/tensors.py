@@ -1,0 +1,81 @@
+"""Small tensor-conversion helpers shared by the model and optimizer layers."""
+from __future__ import annotations
+
+from typing import Any, Optional
+
+import numpy as np
+import torch
+
+__all__ = ["as_param_tensor", "to_numpy", "infer_device", "detach_tree"]
+
+
+def as_param_tensor(x: Any, device=None, dtype: Optional[torch.dtype] = None) -> torch.Tensor:
+    """Convert parameters (tuple/NamedTuple/list/ndarray/tensor) to a 1-d-or-more tensor.
+
+    Floating tensors keep their dtype unless ``dtype`` is given; everything else becomes
+    ``dtype`` (default float32, the reference's JAX default precision).
+    """
+    if isinstance(x, torch.Tensor):
+        t = x
+        if dtype is not None and t.dtype != dtype:
+            t = t.to(dtype)
+        elif not t.is_floating_point():
+            t = t.to(torch.float32)
+    else:
+        if isinstance(x, (list, tuple)) and any(isinstance(v, torch.Tensor) for v in x):
+            t = torch.stack([torch.as_tensor(v) for v in x])
+            if not t.is_floating_point():
+                t = t.to(torch.float32)
+            if dtype is not None:
+                t = t.to(dtype)
+        else:
+            arr = np.asarray(x, dtype=np.float64)
+            t = torch.as_tensor(arr, dtype=dtype or torch.float32)
+    if device is not None and t.device != torch.device(device):
+        t = t.to(device)
+    return t
+
+
+def to_numpy(x: Any) -> np.ndarray:
+    if isinstance(x, torch.Tensor):
+        return x.detach().cpu().numpy()
+    return np.asarray(x)
+
+
+def infer_device(obj: Any, default="cpu") -> torch.device:
+    """First tensor device found in ``obj`` (tensor, dict, list/tuple, dataclass fields)."""
+    seen = 0
+
+    def walk(o):
+        nonlocal seen
+        seen += 1
+        if seen > 10000:
+            return None
+        if isinstance(o, torch.Tensor):
+            return o.device
+        if isinstance(o, dict):
+            for v in o.values():
+                d = walk(v)
+                if d is not None:
+                    return d
+        elif isinstance(o, (list, tuple)):
+            for v in o:
+                d = walk(v)
+                if d is not None:
+                    return d
+        return None
+
+    d = walk(obj)
+    return d if d is not None else torch.device(default)
+
+
+def detach_tree(x: Any) -> Any:
+    if isinstance(x, torch.Tensor):
+        return x.detach()
+    if isinstance(x, tuple) and hasattr(x, "_fields"):
+        return type(x)(*(detach_tree(v) for v in x))
+    if isinstance(x, (list, tuple)):
+        return type(x)(detach_tree(v) for v in x)
+    if isinstance(x, dict):
+        return {k: detach_tree(v) for k, v in x.items()}
+    return x
