@@ -110,10 +110,20 @@ class PopulationShard:
             counts = torch.tensor([self.n], dtype=torch.int64)
             self.pop = None
         else:
-            pop_cpu = torch.as_tensor(pop).reshape(-1).to("cpu", torch.int32).contiguous()
-            order, counts = _sort_by_population(pop_cpu, self.npop)
-            xs = x.reshape(-1)[order.to(x.device)].to(device=device, dtype=torch.float32).contiguous()
-            self.pop = pop_cpu[order].to(device).contiguous()
+            pop = torch.as_tensor(pop).reshape(-1)
+            if pop.device.type == "cuda":
+                # device radix sort + histogram; only the J counts come back to the host
+                spop, order = torch.sort(pop.to(torch.int32), stable=True)
+                counts = torch.bincount(spop, minlength=self.npop).cpu().to(torch.int64)
+                xs = x.reshape(-1).to(pop.device)[order].to(device=device, dtype=torch.float32)
+                self.pop = spop.to(device).contiguous()
+                del order
+            else:
+                pop_cpu = pop.to("cpu", torch.int32).contiguous()
+                order, counts = _sort_by_population(pop_cpu, self.npop)
+                xs = x.reshape(-1)[order.to(x.device)].to(device=device, dtype=torch.float32)
+                self.pop = pop_cpu[order].to(device).contiguous()
+            xs = xs.contiguous()
         self.x = xs
         self.counts = counts
         self.offsets = torch.zeros(self.npop + 1, dtype=torch.int64)

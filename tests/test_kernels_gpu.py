@@ -1,0 +1,182 @@
+"""HIP kernel numerics vs plain PyTorch fp64/fp32 references (run on an MI355X)."""
+import numpy as np
+import pytest
+import torch
+
+from multigrad_amd.ops import smf as S
+from multigrad_amd.ops._schedule import build_tiles_py
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _rand_shard(n, npop, seed=0, giant=None, device=DEV):
+    g = torch.Generator().manual_seed(seed)
+    x = 10.0 + torch.rand(n, generator=g, dtype=torch.float64)
+    pop = torch.randint(0, npop, (n,), generator=g)
+    if giant is not None:  # make one population huge (> tile) to exercise partial tiles
+        pop[: n // 2] = giant
+    return x, pop
+
+
+def _theta(npop, seed=1, dtype=torch.float64):
+    g = torch.Generator().manual_seed(seed)
+    th = torch.empty(2 * npop, dtype=dtype)
+    th[0::2] = -2.0 + 0.2 * (torch.rand(npop, generator=g, dtype=dtype) - 0.5)
+    th[1::2] = -0.5 + 0.2 * (torch.rand(npop, generator=g, dtype=dtype) - 0.5)
+    return th
+
+
+@pytest.mark.parametrize("nbins", [10, 7, 3])
+@pytest.mark.parametrize("giant", [None, 3])
+def test_population_forward_and_vjp_match_fp64(nbins, giant):
+    n, npop = 200_000, 300
+    x, pop = _rand_shard(n, npop, giant=giant)
+    theta64 = _theta(npop)
+    bins = S.SmfBins.make(np.linspace(8.0, 9.6, nbins + 1), volume=1e4)
+    shard = S.PopulationShard(x.float(), pop.int().to(DEV), npop, device=DEV, chunks=3)
+    # fp64 oracle on the same (float32-rounded) inputs
+    xf = x.float().double()
+    th_ref = theta64.float().double().requires_grad_(True)
+    ref = S.smf_sumstats_reference(th_ref, xf, pop, bins, log_sigma=True)
+    gS = torch.linspace(0.5, 1.5, nbins, dtype=torch.float64)
+    (gref,) = torch.autograd.grad(ref, th_ref, gS)
+    th = theta64.float().to(DEV).requires_grad_(True)
+    out = S.smf_sumstats(th, shard, bins, log_sigma=True)
+    (gk,) = torch.autograd.grad(out, th, gS.float().to(DEV))
+    np.testing.assert_allclose(out.detach().cpu().double(), ref.detach(), rtol=2e-5, atol=1e-12)
+    np.testing.assert_allclose(gk.cpu().double(), gref, rtol=2e-4,
+                               atol=2e-5 * float(gref.abs().max()))
+
+
+@pytest.mark.parametrize("log_sigma", [False, True])
+def test_shared_params_model_kernel(log_sigma):
+    n = 300_001
+    x = 10.0 + 0.5 * torch.rand(n, dtype=torch.float64, generator=torch.Generator().manual_seed(3))
+    bins = S.SmfBins.make(np.linspace(9, 10, 11), volume=10.0 * n)
+    th64 = torch.tensor([-1.7, -0.6 if log_sigma else 0.25], dtype=torch.float64)
+    shard = S.PopulationShard(x.float(), None, 1, device=DEV)
+    thr = th64.clone().requires_grad_(True)
+    ref = S.smf_sumstats_reference(thr, x.float().double(), None, bins, log_sigma)
+    (gref,) = torch.autograd.grad(ref.sum(), thr)
+    th = th64.float().to(DEV).requires_grad_(True)
+    out = S.smf_sumstats(th, shard, bins, log_sigma)
+    (gk,) = torch.autograd.grad(out.sum(), th)
+    np.testing.assert_allclose(out.detach().cpu().double(), ref.detach(), rtol=2e-5)
+    np.testing.assert_allclose(gk.cpu().double(), gref, rtol=5e-5)
+
+
+def test_forward_is_deterministic_and_chunks_sum():
+    n, npop = 100_000, 500
+    x, pop = _rand_shard(n, npop, seed=5)
+    shard = S.PopulationShard(x.float(), pop.int().to(DEV), npop, device=DEV, chunks=4)
+    th = _theta(npop).float().to(DEV)
+    bins = S.SmfBins.make(np.linspace(8.0, 9.6, 11), volume=1e4)
+    a = S.smf_sumstats(th, shard, bins)
+    b = S.smf_sumstats(th, shard, bins)
+    assert torch.equal(a, b)
+    parts = torch.zeros(bins.nbp, device=DEV)
+    for c in range(shard.nchunks):
+        o = torch.zeros(bins.nbp, device=DEV)
+        S.smf_forward_into(th, shard, bins, True, o, chunk=c)
+        parts += o
+    torch.testing.assert_close(parts[:10], a, rtol=1e-5, atol=0)
+    # per-chunk VJPs write disjoint parameter ranges that reassemble the full VJP
+    h = torch.randn(bins.nbp + 1, device=DEV)
+    full = torch.zeros(2 * npop, device=DEV)
+    S.smf_vjp_into(th, shard, bins, True, h, full)
+    acc = torch.full((2 * npop,), float("nan"), device=DEV)
+    for c in range(shard.nchunks):
+        S.smf_vjp_into(th, shard, bins, True, h, acc, chunk=c)
+    assert torch.equal(acc, full)
+
+
+def test_tile_schedule_native_matches_python():
+    from multigrad_amd.ops._ext import ext
+    g = torch.Generator().manual_seed(0)
+    counts = torch.randint(0, 40, (5000,), generator=g)
+    counts[100] = 9000
+    counts[4000] = 2049
+    counts[200:260] = 0
+    for breaks in ([], [1000, 2500], [100, 101, 4000]):
+        a = ext().build_tiles(counts.long(), breaks, 2048, 2048)
+        b = build_tiles_py(counts, breaks, 2048, 2048)
+        for x, y in zip(a[:4], b[:4]):
+            assert torch.equal(x.cpu(), y.cpu())
+        assert a[4] == b[4]
+
+
+def test_fused_adam_matches_reference():
+    from multigrad_amd.ops.adam import adam_reference_, fused_adam_
+    from multigrad_amd.optim.transforms import Bounds
+    torch.manual_seed(0)
+    n = 1_000_003  # odd size: vector body + scalar tail
+    u = torch.randn(n, device=DEV)
+    m = torch.zeros(n, device=DEV)
+    v = torch.zeros(n, device=DEV)
+    ur, mr, vr = u.clone(), m.clone(), v.clone()
+    step = torch.zeros(2, dtype=torch.int32, device=DEV)
+    traj = torch.zeros(4, n, device=DEV)
+    for i in range(3):
+        g = torch.randn(n, device=DEV)
+        fused_adam_(u, m, v, g, None, step, 1e-2, 0.9, 0.999, 1e-8, traj_base=traj.reshape(-1),
+                    traj_stride=n)
+        adam_reference_(ur, mr, vr, g, i, 1e-2, 0.9, 0.999, 1e-8)
+    assert step.tolist() == [3, 0]
+    torch.testing.assert_close(u, ur, rtol=1e-6, atol=1e-6)
+    torch.testing.assert_close(m, mr, rtol=1e-6, atol=1e-7)
+    torch.testing.assert_close(traj[3], u)
+    # bounded variant vs the torch Adam implementation
+    from multigrad_amd.optim.adam import Adam
+    nb = 4097
+    spec = [(-1.0, 2.0) if i % 4 == 0 else (0.0, None) if i % 4 == 1 else (None, 3.0)
+            if i % 4 == 2 else None for i in range(nb)]
+    p0 = torch.rand(nb, device=DEV) * 0.9 + 0.05
+    for legacy in (False, True):
+        b = Bounds.from_spec(spec, nb, device=DEV)
+        fa = Adam(p0, 0.05, bounds=b, legacy_bounds_jacobian=legacy)
+        ta = Adam(p0, 0.05, bounds=b, legacy_bounds_jacobian=legacy)
+        ta.fused = False
+        assert fa.fused
+        for _ in range(5):
+            g = torch.randn(nb, device=DEV)
+            fa.update(g)
+            ta.update(g)
+        torch.testing.assert_close(fa.params(), ta.params(), rtol=2e-5, atol=2e-6)
+
+
+def test_engine_matches_generic_adam():
+    from multigrad_amd.models.population import PopulationSMFModel, make_population_data
+    data = make_population_data(num_params=4000, num_halos=200_000, seed=3, device=DEV)
+    model = PopulationSMFModel(aux_data=data)
+    model.set_target_from_truth()
+    t_gen = model.run_adam(data["guess"], nsteps=4, learning_rate=1e-3, use_engine=False)
+    for graph in (False, True):
+        eng = model.fused_engine(graph=graph)
+        t_eng = eng.run_adam(data["guess"], nsteps=4, learning_rate=1e-3)
+        torch.testing.assert_close(t_eng, t_gen, rtol=1e-5, atol=1e-6)
+    loss = model.calc_loss_from_params(t_gen[-1])
+    loss0 = model.calc_loss_from_params(t_gen[0])
+    assert float(loss) < float(loss0)
+
+
+def test_reference_pipeline_on_gpu():
+    """Reference tests/test_mpi.py::test_simple_grad_descent_pipeline on the HIP path."""
+    from multigrad_amd.models.smf import MySMFModel, ParamTuple, TARGET_SUMSTATS, make_test_data
+    data = make_test_data()
+    model = MySMFModel(aux_data=data, device=DEV)
+    truth = ParamTuple(-2.0, 0.2)
+    s = model.calc_sumstats_from_params(truth)
+    assert s.is_cuda
+    np.testing.assert_allclose(s.cpu().numpy(), TARGET_SUMSTATS, rtol=5e-5, atol=1e-9)
+    # self-consistent target (the reference target is itself a float32 JAX evaluation)
+    data["target_sumstats"] = s.cpu().numpy()
+    model = MySMFModel(aux_data=data, device=DEV)
+    gd = model.run_simple_grad_descent(guess=truth, nsteps=2)
+    assert abs(float(gd.loss[-1])) < 1e-10
+    torch.testing.assert_close(gd.params[-1].cpu(), torch.tensor([*truth]), rtol=0, atol=1e-6)
+    assert torch.allclose(model.calc_dloss_dparams(truth).cpu(), torch.zeros(2), atol=1e-5)
+    loss, grad = model.calc_loss_and_grad_from_params(truth)
+    assert torch.allclose(loss, model.calc_loss_from_params(truth))
+    assert torch.allclose(grad, model.calc_dloss_dparams(truth))
