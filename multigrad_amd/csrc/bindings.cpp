@@ -7,6 +7,7 @@
 namespace mg {
 // smf.hip
 int smf_padded_bins(int64_t nb);
+int64_t smf_fwd_max_blocks(int64_t nb, bool log_sigma, bool has_pop);
 void smf_forward(torch::Tensor x, c10::optional<torch::Tensor> pop, torch::Tensor theta,
                  std::vector<double> edges, std::vector<double> scale, bool log_sigma,
                  int64_t begin, int64_t end, torch::Tensor slab, int64_t nblocks);
@@ -38,6 +39,7 @@ PYBIND11_MODULE(_C, m) {
   m.doc() = "multigrad_amd native extension (gfx950 HIP kernels + host runtime)";
   m.def("smf_padded_bins", &mg::smf_padded_bins);
   m.def("smf_forward", &mg::smf_forward);
+  m.def("smf_fwd_max_blocks", &mg::smf_fwd_max_blocks);
   m.def("smf_slab_reduce", &mg::smf_slab_reduce);
   m.def("smf_edge_weights", &mg::smf_edge_weights);
   m.def("smf_logmse", &mg::smf_logmse);

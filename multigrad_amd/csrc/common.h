@@ -46,33 +46,34 @@ __device__ __forceinline__ void block_sum_n(T (&v)[N], T* scratch) {
 __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 __device__ __forceinline__ float fast_rcp(float x) { return __builtin_amdgcn_rcpf(x); }
 
-// Upper-tail normal probability Q(|z|) = P(Z > |z|) = erfc(|z|/sqrt2)/2, accurate to a
-// few ulp *relative* in the far tail (so bin masses far from the mean keep their
-// precision; 0.5*(1+erf) loses it).  Shepherd-Laframboise form: with a = |z|/sqrt2 and
-// q = (a-2)/(a+2), (1+2a) exp(a^2) erfc(a) is a smooth function of q in [-1, 1); it is
-// fitted here by a degree-10 polynomial (coefficients include the factor 1/2).
-// One reciprocal + one exp2 per call.
-__device__ __forceinline__ float normal_tail(float z) {
-  // (clamped: beyond a = 16 exp(-a^2) is 0 and the rational part must stay finite)
-  const float a = fminf(fabsf(z) * 0.70710678118654752f, 16.0f);
-  const float ap2 = a + 2.0f;
-  const float tp1 = fmaf(2.0f, a, 1.0f);
-  const float r = fast_rcp(ap2 * tp1);  // 1 / ((a+2)(1+2a))
-  const float q = (a - 2.0f) * tp1 * r;
-  float p = 0x1.5139fap-14f;
-  p = fmaf(p, q, -0x1.8126a8p-14f);
-  p = fmaf(p, q, -0x1.6de016p-11f);
-  p = fmaf(p, q, 0x1.11743cp-11f);
-  p = fmaf(p, q, 0x1.1cb9eep-8f);
-  p = fmaf(p, q, -0x1.044460p-8f);
-  p = fmaf(p, q, -0x1.bc1ab8p-6f);
-  p = fmaf(p, q, 0x1.4ff206p-4f);
-  p = fmaf(p, q, -0x1.54081cp-4f);
-  p = fmaf(p, q, -0x1.7bf524p-5f);
-  p = fmaf(p, q, 0x1.46e80ep-1f);
-  // exp(-a^2) = exp2(-z^2 * log2(e) / 2)
-  const float e = fast_exp2(z * z * -0.72134752044448170f);
-  return p * ap2 * r * e;
+// Scaled normal coordinate used by the SMF kernels: w = z * kWScale with
+// kWScale = sqrt(log2(e)/2), so that the Gaussian kernel exp(-z^2/2) = exp2(-w^2) costs
+// one multiply + one v_exp_f32.
+constexpr float kWScale = 0x1.b2da4ep-1f;  // 0.84932180
+
+// Upper-tail normal probability Q(|z|) = P(Z > |z|) = erfc(|z|/sqrt2)/2 from the scaled
+// coordinate w, accurate to ~5e-7 *relative* everywhere (including the far tail, where
+// 0.5*(1+erf) loses all precision).  With a = |z|/sqrt2 and q = (a-K)/(a+K), K = 2.5,
+// erfcx(a) = exp(a^2) erfc(a) is a smooth function of q in [-1, 1): a degree-9 minimax
+// polynomial (coefficients fitted offline, they include the factor 1/2).  q is formed
+// directly from b = |w| = a*sqrt(log2 e) (homogeneous), so one v_rcp + one v_exp + 13
+// VALU per call, branch free, NaN only for NaN input.
+__device__ __forceinline__ float normal_tail_w(float w) {
+  constexpr float kKs = 0x1.805bf2p+1f;  // K * sqrt(log2 e) = 3.00280602
+  // q = (b-K)/(b+K) = 1 - 2K/(b+K): one rcp + one fma, finite for b = inf (q -> 1)
+  const float r = fast_rcp(fabsf(w) + kKs);
+  const float q = fmaf(-2.0f * kKs, r, 1.0f);
+  float p = -0x1.9bba2ap-15f;
+  p = fmaf(p, q, 0x1.6288b6p-14f);
+  p = fmaf(p, q, 0x1.c3390ap-12f);
+  p = fmaf(p, q, -0x1.54b8b8p-10f);
+  p = fmaf(p, q, -0x1.05c212p-9f);
+  p = fmaf(p, q, 0x1.46f0a8p-6f);
+  p = fmaf(p, q, -0x1.001088p-4f);
+  p = fmaf(p, q, 0x1.01c172p-3f);
+  p = fmaf(p, q, -0x1.7ca898p-3f);
+  p = fmaf(p, q, 0x1.afbb3cp-4f);
+  return p * fast_exp2(-w * w);
 }
 
 }  // namespace mg

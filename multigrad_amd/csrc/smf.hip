@@ -24,6 +24,7 @@
 
 #include <torch/extension.h>
 #include <ATen/hip/HIPContext.h>
+#include <cmath>
 #include <vector>
 
 namespace mg {
@@ -39,6 +40,7 @@ constexpr float kLog2_10 = 3.321928094887362f;
 struct SmfBins {
   float edge[kMaxBins + 1];  // NBP+1 edges (padded bins are zero width, scale 0)
   float scale[kMaxBins];     // 1 / (volume * width) per bin
+  float delta;               // edge spacing when uniform (== 0: non-uniform)
 };
 
 struct Tile {
@@ -54,40 +56,72 @@ __device__ __forceinline__ float inv_sigma(float s) {
 }
 
 // Accumulate the NB bin masses of one halo.
+// Work with the negated scaled coordinate n_e = -w_e = (mu - e_e) * kWScale / sigma.
+// With signed tails V_e = copysign(Q(|z_e|), n_e) and pos_e = [n_e < 0] = [z_e > 0]
+// (sign bit of n), Phi(z_e) = pos_e + V_e, so mass_k = (V_{k+1} - V_k) + (pos_{k+1} -
+// pos_k): the float part never cancels (tail differences) and the 0/1 part is
+// accumulated exactly as per-edge integer counts, folded in once per thread at the end.
+// A halo with x = -inf contributes exactly zero (used to mask the unrolled tail).
 template <int NB, bool LOGSIG>
-__device__ __forceinline__ void halo_mass(float x, float2 th, const SmfBins& b, float (&acc)[NB]) {
-  const float inv = inv_sigma<LOGSIG>(th.y);
-  const float nmi = -(x + th.x) * inv;  // -mu/sigma
-  float zp = fmaf(b.edge[0], inv, nmi);
-  float tp = normal_tail(zp);
+__device__ __forceinline__ void halo_mass(float x, float2 th, const SmfBins& b, float (&acc)[NB],
+                                          int (&cnt)[NB + 1]) {
+  const float ninv = -inv_sigma<LOGSIG>(th.y) * kWScale;
+  const float mu = -(x + th.x) * ninv;  // = (x + a) * kWScale / sigma
+  float np = fmaf(b.edge[0], ninv, mu);
+  float vp = __builtin_copysignf(normal_tail_w(np), np);
+  cnt[0] += (int)(__float_as_uint(np) >> 31);
 #pragma unroll
   for (int k = 0; k < NB; ++k) {
-    const float z = fmaf(b.edge[k + 1], inv, nmi);
-    const float t = normal_tail(z);
-    // mass of (zp, z]: both tails on the same side -> difference of tails (no
-    // cancellation); straddling the mean -> 1 - both tails.
-    const float m = zp >= 0.0f ? tp - t : (z <= 0.0f ? t - tp : (1.0f - tp) - t);
-    acc[k] += m;
-    zp = z;
-    tp = t;
+    const float n = fmaf(b.edge[k + 1], ninv, mu);
+    const float v = __builtin_copysignf(normal_tail_w(n), n);
+    cnt[k + 1] += (int)(__float_as_uint(n) >> 31);
+    acc[k] += v - vp;
+    vp = v;
   }
 }
 
+// Forward tunables (halos per thread per iteration; minimum resident waves per SIMD).
+#ifndef MG_FWD_UNROLL
+#define MG_FWD_UNROLL 2
+#endif
+#ifndef MG_FWD_MINWAVES
+#define MG_FWD_MINWAVES 8
+#endif
+constexpr int kFwdUnroll = MG_FWD_UNROLL;
+
 template <int NB, bool LOGSIG, bool HAS_POP>
-__global__ __launch_bounds__(kThreads) void smf_fwd_kernel(
+__global__ __launch_bounds__(kThreads, MG_FWD_MINWAVES) void smf_fwd_kernel(
     const float* __restrict__ x, const int32_t* __restrict__ pop,
     const float2* __restrict__ theta, int64_t begin, int64_t end, SmfBins bins,
     float* __restrict__ slab) {
   float acc[NB];
+  int cnt[NB + 1];
 #pragma unroll
   for (int k = 0; k < NB; ++k) acc[k] = 0.0f;
+#pragma unroll
+  for (int k = 0; k <= NB; ++k) cnt[k] = 0;
   const float2 th0 = HAS_POP ? make_float2(0.f, 0.f) : theta[0];
   const int64_t stride = (int64_t)gridDim.x * kThreads;
-  for (int64_t i = begin + (int64_t)blockIdx.x * kThreads + threadIdx.x; i < end; i += stride) {
-    const float xi = x[i];
-    const float2 th = HAS_POP ? theta[pop[i]] : th0;
-    halo_mass<NB, LOGSIG>(xi, th, bins, acc);
+  for (int64_t i0 = begin + (int64_t)blockIdx.x * kThreads + threadIdx.x; i0 < end;
+       i0 += kFwdUnroll * stride) {
+    // issue every load of this iteration before any math (one dependent round trip)
+    float xs[kFwdUnroll];
+    int ps[kFwdUnroll];
+    float2 ths[kFwdUnroll];
+#pragma unroll
+    for (int u = 0; u < kFwdUnroll; ++u) {
+      const int64_t i = i0 + u * stride;
+      const bool ok = i < end;
+      xs[u] = ok ? x[i] : -INFINITY;  // -inf: exactly zero contribution, no branch
+      ps[u] = (HAS_POP && ok) ? pop[i] : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < kFwdUnroll; ++u) ths[u] = HAS_POP ? theta[ps[u]] : th0;
+#pragma unroll
+    for (int u = 0; u < kFwdUnroll; ++u) halo_mass<NB, LOGSIG>(xs[u], ths[u], bins, acc, cnt);
   }
+#pragma unroll
+  for (int k = 0; k < NB; ++k) acc[k] += (float)(cnt[k + 1] - cnt[k]);
   __shared__ float scratch[NB * (kThreads / kWave)];
   block_sum_n<NB>(acc, scratch);
   if (threadIdx.x == 0) {
@@ -97,18 +131,16 @@ __global__ __launch_bounds__(kThreads) void smf_fwd_kernel(
 }
 
 // Sum nrows slab rows per bin in a fixed order (double accumulation), apply the bin
-// scale, write (or add into) out[NB].
+// scale, write out[bin].  One workgroup per bin.
 __global__ __launch_bounds__(kThreads) void slab_reduce_kernel(
     const float* __restrict__ slab, int nrows, int nb, SmfBins bins, float* __restrict__ out) {
   __shared__ double scratch[kThreads / kWave];
-  for (int k = 0; k < nb; ++k) {
-    double s = 0.0;
-    for (int r = threadIdx.x; r < nrows; r += kThreads) s += (double)slab[(int64_t)r * nb + k];
-    double v[1] = {s};
-    block_sum_n<1>(v, scratch);
-    if (threadIdx.x == 0) out[k] = (float)(v[0] * (double)bins.scale[k]);
-    __syncthreads();
-  }
+  const int k = blockIdx.x;
+  double s = 0.0;
+  for (int r = threadIdx.x; r < nrows; r += kThreads) s += (double)slab[(int64_t)r * nb + k];
+  double v[1] = {s};
+  block_sum_n<1>(v, scratch);
+  if (threadIdx.x == 0) out[k] = (float)(v[0] * (double)bins.scale[k]);
 }
 
 // Edge weights h_e from the sumstat cotangent g (dL/dS), folded with 1/sqrt(2 pi).
@@ -150,23 +182,28 @@ __global__ void logmse_loss_kernel(const float* __restrict__ S, const float* __r
   if (k <= nb && h) h[k] = edge_weight(g, bins, k, nb);
 }
 
+// Per-halo VJP contributions in the scaled coordinate w = z*kWScale:
+//   A += sum_e h_e exp2(-w_e^2),   B += sum_e h_e exp2(-w_e^2) w_e
+// (h_e already carries 1/sqrt(2 pi); B is converted back to z units in pop_grad).
 template <int NB, bool LOGSIG>
 __device__ __forceinline__ void halo_vjp(float x, float2 th, float inv, const float (&h)[NB + 1],
                                          const SmfBins& b, float& A, float& B) {
   const float nmi = -(x + th.x) * inv;
 #pragma unroll
   for (int e = 0; e <= NB; ++e) {
-    const float z = fmaf(b.edge[e], inv, nmi);
-    const float w = h[e] * fast_exp2(z * z * -0.72134752044448170f);
-    A += w;
-    B = fmaf(w, z, B);
+    const float w = fmaf(b.edge[e], inv, nmi);
+    const float t = h[e] * fast_exp2(-w * w);
+    A += t;
+    B = fmaf(t, w, B);
   }
 }
 
+// inv is the scaled inverse sigma (kWScale / sigma); A, B from halo_vjp.
 template <bool LOGSIG>
 __device__ __forceinline__ float2 pop_grad(float2 th, float A, float B) {
+  constexpr float kInvW = 1.0f / kWScale;
   const float inv = inv_sigma<LOGSIG>(th.y);
-  return make_float2(-inv * A, LOGSIG ? -kLn10 * B : -inv * B);
+  return make_float2(-inv * A, LOGSIG ? -(kLn10 * kInvW) * B : -(inv * kInvW) * B);
 }
 
 // Segmented-scan combine: (flag, A, B) pairs.
@@ -191,47 +228,88 @@ __global__ __launch_bounds__(kThreads) void smf_vjp_tiles_kernel(
 
   if (t.slot >= 0) {  // partial tile: one population, plain block reduction
     const float2 th = theta[t.p0];
-    const float inv = inv_sigma<LOGSIG>(th.y);
+    const float inv = inv_sigma<LOGSIG>(th.y) * kWScale;
     float v[2] = {0.0f, 0.0f};
-    for (int64_t i = t.h0 + tid; i < t.h1; i += kThreads) halo_vjp<NB, LOGSIG>(x[i], th, inv, h, bins, v[0], v[1]);
+    for (int64_t i0 = t.h0 + tid; i0 < t.h1; i0 += 4 * kThreads) {
+      float xs[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) xs[u] = i0 + u * kThreads < t.h1 ? x[i0 + u * kThreads] : 0.f;
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (i0 + u * kThreads < t.h1) halo_vjp<NB, LOGSIG>(xs[u], th, inv, h, bins, v[0], v[1]);
+    }
     __shared__ float scratch[2 * (kThreads / kWave)];
     block_sum_n<2>(v, scratch);
     if (tid == 0) partials[t.slot] = make_float2(v[0], v[1]);
     return;
   }
 
-  __shared__ float2 res[kTilePops];
+  // LDS: per-halo (A, B) contributions, later re-used as the per-population result
+  // array (kTileHalos == kTilePops), local population ids, and the scan scratch.
+  __shared__ float2 s_ab[kTileHalos];
+  __shared__ int16_t s_lp[kTileHalos];
   __shared__ int s_tailpop[kThreads];
   __shared__ int s_headpop[kThreads];
   __shared__ float2 s_incl[kThreads];
   __shared__ Seg s_wagg[kThreads / kWave];
+  float2* res = s_ab;
+  static_assert(kTileHalos == kTilePops, "result array aliases the contribution array");
 
+  // ---- phase 1: coalesced loads (all rounds issued up front), per-halo contributions
+  {
+    float xs[kItems];
+    int ps[kItems];
+    float2 ths[kItems];
+#pragma unroll
+    for (int r = 0; r < kItems; ++r) {
+      const int64_t i = t.h0 + r * kThreads + tid;
+      const bool ok = i < t.h1;
+      xs[r] = ok ? x[i] : 0.0f;
+      ps[r] = ok ? pop[i] : t.p0;
+    }
+#pragma unroll
+    for (int r = 0; r < kItems; ++r) ths[r] = theta[ps[r]];
+#pragma unroll
+    for (int r = 0; r < kItems; ++r) {
+      float A = 0.f, B = 0.f;
+      const float inv = inv_sigma<LOGSIG>(ths[r].y) * kWScale;
+      halo_vjp<NB, LOGSIG>(xs[r], ths[r], inv, h, bins, A, B);
+      s_ab[r * kThreads + tid] = make_float2(A, B);
+      s_lp[r * kThreads + tid] = (int16_t)(ps[r] - t.p0);
+    }
+  }
+  __syncthreads();
+  // ---- phase 2: blocked per-thread sequential segmented reduction over <= kItems halos
+  const int base = tid * kItems;
+  const int cnt = (int)max((int64_t)0, min((int64_t)kItems, (t.h1 - t.h0) - base));
+  float2 ab[kItems];
+  int lp[kItems];
+#pragma unroll
+  for (int j = 0; j < kItems; ++j) {
+    ab[j] = s_ab[base + j];
+    lp[j] = s_lp[base + j];
+  }
+  __syncthreads();  // contributions are in registers: s_ab becomes res
   const int npops = t.p1 - t.p0;
   for (int k = tid; k < npops; k += kThreads) res[k] = make_float2(0.f, 0.f);
-
-  // ---- blocked per-thread sequential segmented reduction over <= kItems halos
-  const int64_t base = t.h0 + (int64_t)tid * kItems;
-  const int cnt = (int)max((int64_t)0, min((int64_t)kItems, t.h1 - base));
-  int headpop = -1, curpop = -1, nseg = 0;
+  __syncthreads();
+  int headpop = -1, curpop = -1, nseg = 0;  // local population ids
   float headA = 0.f, headB = 0.f, curA = 0.f, curB = 0.f;
-  float2 th = make_float2(0.f, 1.f);
-  float inv = 1.0f;
-  __syncthreads();  // res zeroed before any interior write
-  for (int j = 0; j < cnt; ++j) {
-    const int64_t i = base + j;
-    const int c = pop[i];
-    if (c != curpop) {
-      if (nseg == 1) {
-        headpop = curpop; headA = curA; headB = curB;
-      } else if (nseg > 1) {
-        // complete interior segment owned by this thread
-        res[curpop - t.p0] = make_float2(curA, curB);
+#pragma unroll
+  for (int j = 0; j < kItems; ++j) {
+    if (j < cnt) {
+      const int c = lp[j];
+      if (c != curpop) {
+        if (nseg == 1) {
+          headpop = curpop; headA = curA; headB = curB;
+        } else if (nseg > 1) {
+          res[curpop] = make_float2(curA, curB);  // interior segment owned by this thread
+        }
+        curpop = c; curA = 0.f; curB = 0.f; ++nseg;
       }
-      curpop = c; curA = 0.f; curB = 0.f; ++nseg;
-      th = theta[c];
-      inv = inv_sigma<LOGSIG>(th.y);
+      curA += ab[j].x;
+      curB += ab[j].y;
     }
-    halo_vjp<NB, LOGSIG>(x[i], th, inv, h, bins, curA, curB);
   }
   if (nseg == 1) { headpop = curpop; headA = curA; headB = curB; }
   const bool boundary = nseg > 1;
@@ -267,12 +345,12 @@ __global__ __launch_bounds__(kThreads) void smf_vjp_tiles_kernel(
   if (cnt && boundary) {
     float2 carry = make_float2(0.f, 0.f);
     if (tid && prevtail == headpop) carry = s_incl[tid - 1];
-    res[headpop - t.p0] = make_float2(headA + carry.x, headB + carry.y);
+    res[headpop] = make_float2(headA + carry.x, headB + carry.y);
   }
   // tail segment ends here unless the next thread continues it
   if (cnt) {
     const int nexthead = tid + 1 < kThreads ? s_headpop[tid + 1] : -1;
-    if (nexthead != curpop) res[curpop - t.p0] = s_incl[tid];
+    if (nexthead != curpop) res[curpop] = s_incl[tid];
   }
   __syncthreads();
   for (int k = tid; k < npops; k += kThreads) {
@@ -313,7 +391,12 @@ static SmfBins make_bins(const std::vector<double>& edges, const std::vector<dou
   SmfBins b;
   for (int e = 0; e <= kMaxBins; ++e) b.edge[e] = (float)edges[std::min(e, nb)];
   for (int k = 0; k < kMaxBins; ++k) b.scale[k] = k < nb ? (float)scale[k] : 0.0f;
-  (void)nbp;
+  // uniform spacing (the recurrence path also requires no zero-width padded bins)
+  const double d = (edges[nb] - edges[0]) / nb;
+  bool uni = nb == nbp && d > 0;
+  for (int e = 0; e <= nb && uni; ++e)
+    uni = std::fabs(edges[e] - (edges[0] + e * d)) <= 1e-6 * std::max(1.0, std::fabs(edges[e]));
+  b.delta = uni ? (float)d : 0.0f;
   return b;
 }
 
@@ -335,6 +418,23 @@ static void check_dev(const torch::Tensor& t, const char* name, at::ScalarType s
 }
 
 int smf_padded_bins(int64_t nb) { return padded_bins((int)nb); }
+
+// Grid that exactly fills the chip with resident forward workgroups (occupancy x CUs), so
+// the grid-stride loop runs in a single wave of workgroups without a partial tail round.
+int64_t smf_fwd_max_blocks(int64_t nb, bool log_sigma, bool has_pop) {
+  const int nbp = padded_bins((int)nb);
+  int dev = 0;
+  hipGetDevice(&dev);
+  hipDeviceProp_t prop;
+  hipGetDeviceProperties(&prop, dev);
+  int occ = 0;
+  MG_DISPATCH_NB(nbp, {
+    const void* f = log_sigma ? (has_pop ? (const void*)smf_fwd_kernel<NB, true, true> : (const void*)smf_fwd_kernel<NB, true, false>)
+                              : (has_pop ? (const void*)smf_fwd_kernel<NB, false, true> : (const void*)smf_fwd_kernel<NB, false, false>);
+    hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, f, kThreads, 0);
+  });
+  return (int64_t)std::max(1, occ) * prop.multiProcessorCount;
+}
 
 // Forward over halos [begin, end); writes slab[nblocks * NBP].
 void smf_forward(torch::Tensor x, c10::optional<torch::Tensor> pop, torch::Tensor theta,
@@ -380,7 +480,7 @@ void smf_slab_reduce(torch::Tensor slab, int64_t nrows, std::vector<double> edge
   TORCH_CHECK(out.numel() >= nbp, "out too small");
   const SmfBins b = make_bins(edges, scale, nbp);
   auto stream = at::hip::getCurrentHIPStream();
-  hipLaunchKernelGGL(slab_reduce_kernel, dim3(1), dim3(kThreads), 0, stream,
+  hipLaunchKernelGGL(slab_reduce_kernel, dim3(nbp), dim3(kThreads), 0, stream,
                      slab.data_ptr<float>(), (int)nrows, nbp, b, out.data_ptr<float>());
 }
 

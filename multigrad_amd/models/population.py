@@ -155,4 +155,5 @@ class PopulationSMFModel(OnePointModel):
 
     def engine_sizes(self):
         """(nparams, sumstat buffer length, edge-weight buffer length, forward blocks)."""
-        return self.nparams, self.bins.nbp, self.bins.nbp + 1, self.shard.fwd_blocks(max(self.shard.n, 1))
+        return (self.nparams, self.bins.nbp, self.bins.nbp + 1,
+                self.shard.fwd_blocks(max(self.shard.n, 1), self.bins.nb, True))

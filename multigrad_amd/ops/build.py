@@ -20,8 +20,8 @@ from typing import List
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(PKG_DIR, "csrc")
-OBJ_DIR = os.path.join(os.path.dirname(PKG_DIR), "build", "obj")
-TARGET = os.path.join(PKG_DIR, "_C.so")
+OBJ_DIR = os.environ.get("MULTIGRAD_OBJ_DIR", os.path.join(os.path.dirname(PKG_DIR), "build", "obj"))
+TARGET = os.environ.get("MULTIGRAD_TARGET", os.path.join(PKG_DIR, "_C.so"))
 ARCH = os.environ.get("MULTIGRAD_OFFLOAD_ARCH", os.environ.get("PYTORCH_ROCM_ARCH", "gfx950"))
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 
@@ -60,8 +60,9 @@ def _compile_cmd(src: str) -> List[str]:
               "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1", "-Wno-unused-result",
               f"-I{CSRC}", f"-I{py_inc}"] + [f"-I{d}" for d in inc] + [f"-I{ROCM}/include"]
     if src.endswith(".hip"):
+        extra = os.environ.get("MULTIGRAD_HIPCC_FLAGS", "").split()
         return [os.path.join(ROCM, "bin", "hipcc"), "-c", src, "-o", _obj(src),
-                f"--offload-arch={ARCH}", "-ffp-contract=fast"] + common
+                f"--offload-arch={ARCH}", "-ffp-contract=fast"] + common + extra
     return ["g++", "-c", src, "-o", _obj(src)] + common
 
 

@@ -140,8 +140,20 @@ class PopulationShard:
         self.nslots = int(nslots)
         self.partials = torch.zeros(max(self.nslots, 1) * 2, dtype=torch.float32, device=device)
 
-    def fwd_blocks(self, nhalos: int) -> int:
-        return int(max(1, min(FWD_BLOCKS_MAX, math.ceil(nhalos / 256))))
+    def fwd_blocks(self, nhalos: int, nbins: int = 10, log_sigma: bool = True) -> int:
+        """Forward grid: enough 256-thread workgroups for the halos (4 per thread per
+        iteration), capped at one fully resident wave of workgroups."""
+        cap = FWD_BLOCKS_MAX
+        if self.device.type == "cuda":
+            key = (nbins, bool(log_sigma), self.pop is not None)
+            if key not in _GRID_CACHE:
+                _GRID_CACHE[key] = int(ext().smf_fwd_max_blocks(nbins, bool(log_sigma),
+                                                                self.pop is not None))
+            cap = _GRID_CACHE[key]
+        return int(max(1, min(cap, math.ceil(nhalos / 256))))
+
+
+_GRID_CACHE: dict = {}
 
 
 def _sort_by_population(pop_cpu: torch.Tensor, npop: int):
@@ -171,7 +183,7 @@ def smf_forward_into(theta: torch.Tensor, shard: PopulationShard, bins: SmfBins,
         h0, h1 = 0, shard.n
     else:
         h0, h1 = shard.chunk_halos[chunk], shard.chunk_halos[chunk + 1]
-    nblk = shard.fwd_blocks(max(h1 - h0, 1))
+    nblk = shard.fwd_blocks(max(h1 - h0, 1), bins.nb, log_sigma)
     if slab is None:
         slab = torch.empty(nblk * bins.nbp, dtype=torch.float32, device=theta.device)
     E.smf_forward(shard.x, shard.pop, theta, list(bins.edges), list(bins.scale), bool(log_sigma),
