@@ -80,26 +80,34 @@ class Bounds:
                       self.kind.to(device=device))
 
     # ------------------------------------------------------------- vectorised maps
+    def _safe(self, like: torch.Tensor):
+        """Bounds with absent sides replaced by finite dummies, so the branches that
+        ``torch.where`` discards never produce inf/NaN (which would poison gradients)."""
+        k = self.kind.to(like.device)
+        lo = torch.where(torch.isfinite(self.lo), self.lo, torch.zeros_like(self.lo)).to(like)
+        hi = torch.where(torch.isfinite(self.hi), self.hi, torch.ones_like(self.hi)).to(like)
+        both = k == KIND_BOTH
+        mid = torch.where(both, (hi + lo) / 2, torch.zeros_like(lo))
+        s = torch.where(both, (hi - lo) / math.pi, torch.ones_like(lo))
+        return k, lo, hi, mid, s
+
     def forward(self, p: torch.Tensor) -> torch.Tensor:
-        lo, hi, k = self.lo.to(p), self.hi.to(p), self.kind.to(p.device)
-        mid = (hi + lo) / 2
-        s = (hi - lo) / math.pi
+        k, lo, hi, mid, s = self._safe(p)
         both = torch.where(k == KIND_BOTH, s * torch.tan((p - mid) / s), p)
-        low = torch.where(k == KIND_LOW, p - lo + 1.0 / (lo - p), both)
-        return torch.where(k == KIND_HIGH, p - hi + 1.0 / (hi - p), low)
+        dl = torch.where(k == KIND_LOW, lo - p, torch.ones_like(p))
+        low = torch.where(k == KIND_LOW, p - lo + 1.0 / dl, both)
+        dh = torch.where(k == KIND_HIGH, hi - p, torch.ones_like(p))
+        return torch.where(k == KIND_HIGH, p - hi + 1.0 / dh, low)
 
     def inverse(self, u: torch.Tensor) -> torch.Tensor:
-        lo, hi, k = self.lo.to(u), self.hi.to(u), self.kind.to(u.device)
-        mid = (hi + lo) / 2
-        s = (hi - lo) / math.pi
+        k, lo, hi, mid, s = self._safe(u)
         r = torch.sqrt(u * u + 4)
         both = torch.where(k == KIND_BOTH, mid + s * torch.atan(u / s), u)
         low = torch.where(k == KIND_LOW, 0.5 * (2 * lo + u + r), both)
         return torch.where(k == KIND_HIGH, 0.5 * (2 * hi + u - r), low)
 
     def dpdu(self, u: torch.Tensor) -> torch.Tensor:
-        lo, hi, k = self.lo.to(u), self.hi.to(u), self.kind.to(u.device)
-        s = (hi - lo) / math.pi
+        k, lo, hi, mid, s = self._safe(u)
         r = torch.sqrt(u * u + 4)
         one = torch.ones_like(u)
         both = torch.where(k == KIND_BOTH, 1.0 / (1.0 + (u / s) ** 2), one)
