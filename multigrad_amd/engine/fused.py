@@ -1,39 +1,52 @@
-"""Fused, device-resident Adam engine (HIP kernels + stream-ordered collectives).
+"""Fused, device-resident Adam engine (HIP kernels + stream-ordered RCCL collectives).
 
 The generic path (``OnePointModel.run_adam``) runs the distributed chain rule through
 autograd with Python in the loop.  Models that expose the *engine protocol* run instead
 as a fixed sequence of device operations per step, with no host synchronisation:
 
-    partial sumstats  (fwd kernel + deterministic slab reduce)     -> S
-    all-reduce(S)     (RCCL, latency bound, K floats)
-    loss + edge weights from S (1 tiny kernel)                     -> loss, h
-    local VJP         (segmented per-population kernel)            -> g
-    all-reduce(g)     (RCCL, bandwidth bound, P floats) -- or reduce-scatter + all-gather
-                      with the optimizer sharded across ranks (ZeRO-1 style)
-    fused Adam        (1 HBM pass: moments, bias correction, transform, trajectory row)
+    forward per chunk      (HIP kernel -> per-workgroup slab rows)
+    slab reduce            (fixed-order sum)                               -> S
+    all-reduce(S)          (RCCL, latency bound, K floats)
+    loss + edge weights    (1 tiny kernel)                                 -> loss, h
+    VJP per chunk          (segmented per-population kernel)               -> g_c
+    ZeRO-1 (world > 1, default):
+        reduce-scatter(g_c)  issued right after VJP_c on RCCL's stream, so it overlaps
+                             VJP_{c+1} on the compute stream
+        fused Adam on the owned 1/W slice of chunk c (as soon as RS_c lands)
+        all-gather(theta_c)  overlapping Adam_{c+1} and, across the step boundary, the
+                             next step's forward of chunk c-1...
+    replicated (world == 1, or zero=False):
+        all-reduce(g) + fused Adam over every parameter
 
-On a single GPU the whole step is captured once into a HIP graph and replayed
-(``torch.cuda.CUDAGraph``); the device step counter inside the Adam kernel makes the
-replay self-advancing.  This replaces the reference's per-step host round trips
-(4 host crossings per Adam step, 2 of them pickled broadcasts).
+RS + AG move exactly the bytes of one all-reduce, but the optimizer work and the Adam
+state drop to 1/W per GPU and every collective hides behind compute of a neighbouring
+chunk.  Parameters stay bitwise identical across ranks (each slice has one owner).
 
-Engine protocol (see :class:`~multigrad_amd.models.population.PopulationSMFModel`):
-``engine_sizes() -> (P, nS, nH, fwd_blocks)``, ``engine_partial_into(theta, S, slab)``,
-``engine_loss_into(S, loss, h)``, ``engine_vjp_into(theta, h, grad)``.
+On a single GPU the whole step is captured once into a HIP graph and replayed; the
+device step counter inside the Adam kernel makes the replay self-advancing.  This
+replaces the reference's per-step host round trips (4 host crossings per
+Adam step, 2 of them pickled broadcasts).
+
+Engine protocol (implemented by :class:`~multigrad_amd.models.population.PopulationSMFModel`):
+``engine_units() -> (J, params_per_unit)``, ``engine_set_chunks(unit_bounds)``,
+``engine_nS()``, ``engine_fwd_rows(chunk)``, ``engine_forward_chunk(theta, slab, chunk)
+-> rows``, ``engine_reduce(slab, rows, S)``, ``engine_loss_into(S, loss, h)``,
+``engine_vjp_into(theta, h, grad, chunk)``.  Every method works on CPU tensors too
+(PyTorch reference math), which is how the multi-rank orchestration is tested on gloo.
 """
 from __future__ import annotations
 
+import math
 import os
-import time
-from typing import Optional
+from typing import List, Optional
 
 import torch
 
 from ..optim.adam import History
-from ..optim.transforms import Bounds
-from ..ops import adam as adam_ops
+from ..optim.transforms import Bounds, KIND_NONE
+from ..ops.adam import adam_step_
 
-__all__ = ["FusedAdamEngine"]
+__all__ = ["FusedAdamEngine", "plan_chunks"]
 
 
 def _env_flag(name: str, default: Optional[bool]) -> Optional[bool]:
@@ -43,20 +56,48 @@ def _env_flag(name: str, default: Optional[bool]) -> Optional[bool]:
     return v.lower() not in ("0", "false", "off", "no")
 
 
+def plan_chunks(J: int, upp: int, world: int, nchunks: int):
+    """Unit-aligned chunk boundaries whose parameter counts are multiples of 4*world
+    (float4 lanes on every reduce-scatter slice); the last chunk is padded.
+
+    Returns (unit_bounds, param_bounds, P_pad, chunk_lengths)."""
+    q = 4 * world
+    a = q // math.gcd(q, upp)  # units per alignment block
+    C = max(1, min(int(nchunks), J))
+    ub = sorted({min(J, int(round(c * J / C / a)) * a) for c in range(C)} | {0, J})
+    ub = [u for u in ub if u <= J]
+    # drop empty chunks (duplicates already removed); keep J as the final bound
+    pb = [u * upp for u in ub]
+    last = pb[-1] - pb[-2]
+    P_pad = pb[-2] + (-(-last // q) * q if last else 0)
+    lengths = [pb[i + 1] - pb[i] for i in range(len(pb) - 2)] + [P_pad - pb[-2]]
+    return ub, pb, P_pad, lengths
+
+
 class FusedAdamEngine:
     """Device-resident Adam for a model implementing the engine protocol.
 
     Parameters
     ----------
     model : the model (its ``comm`` is used for the collectives)
-    graph : capture the step into a HIP graph (default: on for a single rank; env
+    graph : capture the step into a HIP graph (default: on for a single GPU rank;
         ``MULTIGRAD_GRAPH`` overrides)
+    zero : shard the optimizer across ranks (reduce-scatter / all-gather); default on
+        for more than one rank (``MULTIGRAD_ZERO``)
+    chunks : number of parameter chunks for collective/compute overlap (default 1 on a
+        single rank, 8 otherwise; ``MULTIGRAD_CHUNKS``)
     """
 
-    def __init__(self, model, comm=None, graph: Optional[bool] = None):
+    def __init__(self, model, comm=None, graph: Optional[bool] = None,
+                 zero: Optional[bool] = None, chunks: Optional[int] = None):
         self.model = model
         self.comm = model.comm if comm is None else comm
         self.size = 1 if self.comm is None else self.comm.size
+        self.rank = 0 if self.comm is None else self.comm.rank
+        z = _env_flag("MULTIGRAD_ZERO", zero)
+        self.zero = (self.size > 1) if z is None else bool(z) and self.size > 1
+        nc = chunks if chunks is not None else int(os.environ.get("MULTIGRAD_CHUNKS", "0")) or None
+        self.nchunks_req = nc if nc is not None else (1 if self.size == 1 else 8)
         g = _env_flag("MULTIGRAD_GRAPH", graph)
         self.use_graph = (self.size == 1) if g is None else bool(g)
         self.graph = None
@@ -66,55 +107,161 @@ class FusedAdamEngine:
     def setup(self, guess, nsteps: int, param_bounds=None, learning_rate: float = 0.01,
               b1: float = 0.9, b2: float = 0.999, eps: float = 1e-8, history="full",
               legacy_bounds_jacobian: bool = False):
-        P, nS, nH, nblk = self.model.engine_sizes()
-        dev = self.model.param_device()
+        md = self.model
+        dev = md.param_device()
+        self.device = dev
+        if dev.type != "cuda":
+            self.use_graph = False
+        J, upp = md.engine_units()
+        P = J * upp
+        W = self.size if self.zero else 1
+        ub, pb, P_pad, lengths = plan_chunks(J, upp, W, self.nchunks_req)
+        md.engine_set_chunks(ub)
+        self.P, self.P_pad, self.pb, self.lengths = P, P_pad, pb, lengths
+        self.C = len(lengths)
+        self.lr, self.b1, self.b2, self.eps = float(learning_rate), float(b1), float(b2), float(eps)
+        self.legacy = bool(legacy_bounds_jacobian)
         p0 = torch.as_tensor(guess).detach().reshape(-1).to(device=dev, dtype=torch.float32)
         assert p0.numel() == P, f"guess has {p0.numel()} params, model expects {P}"
-        self.P = P
-        self.lr, self.b1, self.b2, self.eps = float(learning_rate), float(b1), float(b2), float(eps)
-        self.bounds = Bounds.from_spec(param_bounds, P, device=dev)
-        self.legacy = bool(legacy_bounds_jacobian)
-        if self.bounds is not None:
-            self.u = self.bounds.forward(p0).contiguous()
-            self.theta = self.bounds.inverse(self.u).contiguous()
+        f32 = dict(dtype=torch.float32, device=dev)
+        bounds = Bounds.from_spec(param_bounds, P, device=dev)
+        if bounds is not None and P_pad > P:
+            pad = P_pad - P
+            bounds = Bounds(torch.cat([bounds.lo, torch.full((pad,), -math.inf, **f32)]),
+                            torch.cat([bounds.hi, torch.full((pad,), math.inf, **f32)]),
+                            torch.cat([bounds.kind, torch.full((pad,), KIND_NONE, dtype=torch.int8,
+                                                               device=dev)]))
+        self.bounds = bounds
+        theta = torch.zeros(P_pad, **f32)
+        theta[:P] = p0
+        if bounds is not None:  # the recorded start is T^-1(T(guess)), as the reference
+            theta.copy_(bounds.inverse(bounds.forward(theta)))
+        self.theta = theta
+        self.grad = torch.zeros(P_pad, **f32)
+        nS = md.engine_nS()
+        self.nS = nS
+        self.rows = [md.engine_fwd_rows(c) for c in range(self.C)]
+        self.S = torch.zeros(nS, **f32)
+        self.slab = torch.zeros(max(1, sum(self.rows)) * nS, **f32)
+        self.h = torch.zeros(nS + 1, **f32)
+        self.loss = torch.zeros(1, **f32)
+        self.step_dev = torch.zeros((self.C, 2), dtype=torch.int32, device=dev)
+        if self.zero:
+            self.loc_len = [L // W for L in lengths]
+            self.loc_off = [sum(self.loc_len[:c]) for c in range(self.C)]
+            nloc = sum(self.loc_len)
+            self.own = [(pb[c] + self.rank * self.loc_len[c], pb[c] + (self.rank + 1) * self.loc_len[c])
+                        for c in range(self.C)]
+            self.m = torch.zeros(nloc, **f32)
+            self.v = torch.zeros(nloc, **f32)
+            self.g_loc = torch.zeros(nloc, **f32)
+            if bounds is not None:
+                idx = torch.cat([torch.arange(a, b, device=dev) for a, b in self.own])
+                self.bounds_loc = Bounds(bounds.lo[idx].contiguous(), bounds.hi[idx].contiguous(),
+                                         bounds.kind[idx].contiguous())
+                self.u_loc = self.bounds_loc.forward(theta[idx]).contiguous()
+            else:
+                self.bounds_loc = None
+                self.u_loc = None
         else:
-            self.u = p0.clone()
-            self.theta = self.u
-        self.m = torch.zeros_like(self.u)
-        self.v = torch.zeros_like(self.u)
-        self.grad = torch.zeros_like(self.u)
-        self.S = torch.zeros(nS, dtype=torch.float32, device=dev)
-        self.slab = torch.zeros(max(nblk, 1) * nS, dtype=torch.float32, device=dev)
-        self.h = torch.zeros(nH, dtype=torch.float32, device=dev)
-        self.loss = torch.zeros(1, dtype=torch.float32, device=dev)
-        self.step_dev = torch.zeros(2, dtype=torch.int32, device=dev)
+            self.u = bounds.forward(theta).contiguous() if bounds is not None else theta
+            self.m = torch.zeros(P_pad, **f32)
+            self.v = torch.zeros(P_pad, **f32)
         self.step_host = 0
         self.nsteps = int(nsteps)
-        self.history = History(history, nsteps, self.theta.detach().clone())
+        self.history = History(history, nsteps, theta[:P].detach().clone())
+        self._ag: List = [None] * self.C
+        self._ag_row = [None] * self.C
         self.graph = None
         self.ready = True
         return self
 
+    # ------------------------------------------------------------------ helpers
+    def _bslice(self, c):
+        if self.bounds_loc is None:
+            return None
+        o, n = self.loc_off[c], self.loc_len[c]
+        b = self.bounds_loc
+        return Bounds(b.lo[o:o + n], b.hi[o:o + n], b.kind[o:o + n])
+
+    def _drain(self, c):
+        """Wait for chunk c's parameter all-gather and record its trajectory slice."""
+        w = self._ag[c]
+        if w is None:
+            return
+        w.wait()
+        self._ag[c] = None
+        row = self._ag_row[c]
+        if row is not None and self.history.mode == "full":
+            a, b = self.pb[c], min(self.pb[c] + self.lengths[c], self.P)
+            if b > a:
+                self.history.buf[row, a:b].copy_(self.theta[a:b])
+
+    def drain(self):
+        for c in range(self.C):
+            self._drain(c)
+
     # ------------------------------------------------------------------ one step
-    def _enqueue_step(self):
+    def _forward_loss(self):
         md = self.model
-        md.engine_partial_into(self.theta, self.S, slab=self.slab)
+        row = 0
+        for c in range(self.C):
+            self._drain(c)
+            n = md.engine_forward_chunk(self.theta, self.slab[row * self.nS:], c)
+            row += n
+        md.engine_reduce(self.slab, row, self.S)
         if self.size > 1:
             self.comm.all_reduce(self.S)
         md.engine_loss_into(self.S, self.loss, self.h)
-        md.engine_vjp_into(self.theta, self.h, self.grad)
-        if self.size > 1:
-            self.comm.all_reduce(self.grad)
-        traj_base, stride = None, 0
-        if self.history.mode == "full":
-            traj_base, stride = self.history.buf.reshape(-1), self.P
-        adam_ops.fused_adam_(self.u, self.m, self.v, self.grad,
-                             self.theta if self.bounds is not None else None, self.step_dev,
-                             self.lr, self.b1, self.b2, self.eps, self.bounds, self.legacy,
-                             traj_base=traj_base, traj_stride=stride)
+
+    def _enqueue_step(self):
+        md = self.model
+        self._forward_loss()
+        hb = self.history.buf.reshape(-1) if self.history.mode == "full" else None
+        if self.zero:
+            rs = []
+            for c in range(self.C):
+                md.engine_vjp_into(self.theta, self.h, self.grad, chunk=c)
+                a, L = self.pb[c], self.lengths[c]
+                o, n = self.loc_off[c], self.loc_len[c]
+                rs.append(self.comm.reduce_scatter_tensor(self.g_loc[o:o + n], self.grad[a:a + L],
+                                                          async_op=True))
+            for c in range(self.C):
+                rs[c].wait()
+                a, b = self.own[c]
+                o, n = self.loc_off[c], self.loc_len[c]
+                u = self.u_loc[o:o + n] if self.u_loc is not None else self.theta[a:b]
+                p = self.theta[a:b] if self.u_loc is not None else None
+                adam_step_(u, self.m[o:o + n], self.v[o:o + n], self.g_loc[o:o + n], p,
+                           self.step_dev[c], self.lr, self.b1, self.b2, self.eps,
+                           self._bslice(c), self.legacy)
+                pa, L = self.pb[c], self.lengths[c]
+                self._ag[c] = self.comm.all_gather_into_tensor(self.theta[pa:pa + L],
+                                                               self.theta[a:b], async_op=True)
+                self._ag_row[c] = self.step_host + 1
+        else:
+            for c in range(self.C):
+                md.engine_vjp_into(self.theta, self.h, self.grad, chunk=c if self.C > 1 else None)
+            if self.size > 1:
+                self.comm.all_reduce(self.grad)
+            stride = self.P if hb is not None else 0
+            bnd = self.bounds
+            if hb is not None and self.P_pad != self.P:
+                # trajectory rows are P long: update the real parameters and the padding
+                # separately so the kernel writes exactly one row
+                P = self.P
+                adam_step_(self.u[:P], self.m[:P], self.v[:P], self.grad[:P],
+                           self.theta[:P] if bnd is not None else None, self.step_dev[0],
+                           self.lr, self.b1, self.b2, self.eps,
+                           None if bnd is None else Bounds(bnd.lo[:P], bnd.hi[:P], bnd.kind[:P]),
+                           self.legacy, traj_base=hb, traj_stride=stride)
+            else:
+                adam_step_(self.u, self.m, self.v, self.grad,
+                           self.theta if bnd is not None else None, self.step_dev[0],
+                           self.lr, self.b1, self.b2, self.eps, bnd, self.legacy,
+                           traj_base=hb, traj_stride=stride)
 
     def _capture(self):
-        # warm the allocator/stream state on a side stream, then capture one step
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         torch.cuda.current_stream().wait_stream(s)
@@ -123,7 +270,7 @@ class FusedAdamEngine:
             self._enqueue_step()
 
     def step(self):
-        """Enqueue one optimizer step (asynchronous)."""
+        """Enqueue one optimizer step (asynchronous on GPU)."""
         assert self.ready, "call setup() first"
         if self.step_host >= self.nsteps and self.history.mode == "full":
             raise RuntimeError("more steps than the trajectory buffer was sized for")
@@ -135,10 +282,12 @@ class FusedAdamEngine:
             self._enqueue_step()
         self.step_host += 1
         if self.history.mode != "full":
-            self.history.record(self.step_host - 1, self.theta)
+            self.drain()
+            self.history.record(self.step_host - 1, self.theta[:self.P])
 
     def params(self) -> torch.Tensor:
-        return self.theta
+        self.drain()
+        return self.theta[:self.P]
 
     def last_loss(self) -> float:
         return float(self.loss.item())
@@ -154,4 +303,5 @@ class FusedAdamEngine:
             self.step()
             if callback is not None:
                 callback(i, self.loss, self)
+        self.drain()
         return self.history.result()

@@ -24,7 +24,8 @@ from typing import Optional
 import numpy as np
 import torch
 
-from ..ops.smf import (PopulationShard, SmfBins, logmse_loss, smf_forward_into, smf_sumstats,
+from ..ops.smf import (PopulationShard, SmfBins, logmse_loss, smf_edge_weights_into,
+                       smf_forward_into, smf_forward_slab, smf_slab_reduce, smf_sumstats,
                        smf_vjp_into)
 from ..parallel.comm import get_world_comm
 from .onepoint import OnePointModel
@@ -135,25 +136,54 @@ class PopulationSMFModel(OnePointModel):
         return S
 
     # ------------------------------------------------------------ fused-engine protocol
+    # (see multigrad_amd.engine.fused): parameters are grouped in "units" of 2 (one
+    # population); the engine chooses unit-aligned chunk boundaries.
     def fused_engine(self, **kw):
-        if self.param_device().type != "cuda":
-            return None
         from ..engine.fused import FusedAdamEngine
         return FusedAdamEngine(self, **kw)
 
-    def engine_partial_into(self, theta, out, slab=None, chunk=None):
-        return smf_forward_into(theta, self.shard, self.bins, True, out, slab=slab, chunk=chunk)
+    def engine_units(self):
+        """(number of parameter units, parameters per unit)."""
+        return self.aux_data["npop"], 2
+
+    def engine_set_chunks(self, unit_bounds):
+        self.shard.set_chunks(unit_bounds)
+
+    def engine_nS(self) -> int:
+        return self.bins.nbp
+
+    def engine_fwd_rows(self, chunk=None) -> int:
+        if self.shard.device.type != "cuda":
+            return 1
+        h0, h1 = self.shard.halo_range(chunk)
+        return self.shard.fwd_blocks(max(h1 - h0, 1), self.bins.nb, True)
+
+    def engine_forward_chunk(self, theta, slab, chunk=None) -> int:
+        return smf_forward_slab(theta, self.shard, self.bins, True, slab, chunk)
+
+    def engine_reduce(self, slab, nrows, S):
+        return smf_slab_reduce(slab, nrows, self.bins, S)
 
     def engine_loss_into(self, S_total, loss_out, h_out):
-        from ..ops._ext import ext
         t = self.aux_data["target_sumstats"]
-        ext().smf_logmse(S_total, t, float(self.aux_data["loss_eps"]), list(self.bins.edges),
-                         list(self.bins.scale), loss_out, torch.empty(0, device=S_total.device), h_out)
+        eps = float(self.aux_data["loss_eps"])
+        if S_total.device.type != "cuda":
+            s = S_total[:self.bins.nb].detach().double().clone().requires_grad_(True)
+            with torch.enable_grad():
+                loss = logmse_loss(s, t.double(), eps)
+                (g,) = torch.autograd.grad(loss, s)
+            loss_out[0] = loss.detach().to(loss_out.dtype)
+            smf_edge_weights_into(g.float(), self.bins, h_out)
+            return
+        from ..ops._ext import ext
+        if getattr(self, "_empty", None) is None or self._empty.device != S_total.device:
+            self._empty = torch.empty(0, device=S_total.device)
+        ext().smf_logmse(S_total, t, eps, list(self.bins.edges), list(self.bins.scale),
+                         loss_out, self._empty, h_out)
 
     def engine_vjp_into(self, theta, h, grad, chunk=None):
         return smf_vjp_into(theta, self.shard, self.bins, True, h, grad, chunk=chunk)
 
-    def engine_sizes(self):
-        """(nparams, sumstat buffer length, edge-weight buffer length, forward blocks)."""
-        return (self.nparams, self.bins.nbp, self.bins.nbp + 1,
-                self.shard.fwd_blocks(max(self.shard.n, 1), self.bins.nb, True))
+    # simple (unchunked) protocol helpers
+    def engine_partial_into(self, theta, out, slab=None, chunk=None):
+        return smf_forward_into(theta, self.shard, self.bins, True, out, slab=slab, chunk=chunk)

@@ -7,7 +7,7 @@ import torch
 
 from ._ext import ext
 
-__all__ = ["fused_adam_", "adam_reference_"]
+__all__ = ["fused_adam_", "adam_reference_", "adam_step_"]
 
 
 def fused_adam_(u: torch.Tensor, m: torch.Tensor, v: torch.Tensor, g: torch.Tensor,
@@ -43,3 +43,30 @@ def adam_reference_(u, m, v, g, step: int, lr, b1, b2, eps):
     mhat = m / (1 - b1 ** (step + 1))
     vhat = v / (1 - b2 ** (step + 1))
     u.sub_(lr * mhat / (torch.sqrt(vhat) + eps))
+
+
+def adam_step_(u, m, v, g, p, step: torch.Tensor, lr, b1, b2, eps, bounds=None,
+               legacy: bool = False, traj_base=None, traj_stride: int = 0) -> None:
+    """Device-agnostic in-place Adam step: the fused HIP kernel on GPU tensors, the same
+    arithmetic in PyTorch on CPU tensors (``step`` is then a CPU ``[2]`` int tensor)."""
+    if u.device.type == "cuda":
+        fused_adam_(u, m, v, g, p, step, lr, b1, b2, eps, bounds, legacy,
+                    traj_base=traj_base, traj_stride=traj_stride)
+        return
+    i = int(step[0])
+    gg = g
+    if bounds is not None:
+        at = p if legacy else u
+        gg = g * bounds.dpdu(at)
+    m.mul_(b1).add_((1 - b1) * gg)
+    v.mul_(b2).add_((1 - b2) * gg * gg)
+    mhat = m / (1 - b1 ** (i + 1))
+    vhat = v / (1 - b2 ** (i + 1))
+    u.sub_(lr * mhat / (torch.sqrt(vhat) + eps))
+    newp = bounds.inverse(u) if bounds is not None else u
+    if bounds is not None:
+        p.copy_(newp)
+    if traj_base is not None:
+        n = u.numel()
+        traj_base[(i + 1) * traj_stride:(i + 1) * traj_stride + n].copy_(newp)
+    step[0] = i + 1

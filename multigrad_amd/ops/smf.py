@@ -128,17 +128,40 @@ class PopulationShard:
         self.counts = counts
         self.offsets = torch.zeros(self.npop + 1, dtype=torch.int64)
         self.offsets[1:] = torch.cumsum(counts, 0)
-        self.nchunks = max(1, min(int(chunks), self.npop))
-        bounds = np.linspace(0, self.npop, self.nchunks + 1).round().astype(np.int64)
-        self.chunk_pops = [int(b) for b in bounds]
-        self.chunk_halos = [int(self.offsets[b]) for b in bounds]
-        tiles, giant, ct, cg, nslots = _build_tiles(counts, self.chunk_pops[1:-1], tile_halos, tile_pops)
-        self.tiles = tiles.to(device)
-        self.giant = giant.to(device)
+        self._tile_halos, self._tile_pops = tile_halos, tile_pops
+        bounds = np.linspace(0, self.npop, max(1, min(int(chunks), self.npop)) + 1).round()
+        self.set_chunks([int(b) for b in bounds])
+
+    def set_chunks(self, pop_bounds) -> None:
+        """(Re)cut the shard into contiguous population chunks ``[b_c, b_{c+1})`` and
+        rebuild the tile schedule so that no tile straddles a chunk boundary."""
+        pb = [int(b) for b in pop_bounds]
+        assert pb[0] == 0 and pb[-1] == self.npop and all(a <= b for a, b in zip(pb, pb[1:]))
+        self.nchunks = len(pb) - 1
+        self.chunk_pops = pb
+        self.chunk_halos = [int(self.offsets[b]) for b in pb]
+        if self.device.type != "cuda":
+            self.tiles = torch.zeros((0, 4), dtype=torch.int64)
+            self.giant = torch.zeros((0, 3), dtype=torch.int32)
+            self.chunk_tiles = [0] * (self.nchunks + 1)
+            self.chunk_giant = [0] * (self.nchunks + 1)
+            self.nslots = 0
+            self.partials = torch.zeros(2, dtype=torch.float32)
+            return
+        tiles, giant, ct, cg, nslots = _build_tiles(self.counts, pb[1:-1], self._tile_halos,
+                                                    self._tile_pops)
+        self.tiles = tiles.to(self.device)
+        self.giant = giant.to(self.device)
         self.chunk_tiles = [int(v) for v in ct]
         self.chunk_giant = [int(v) for v in cg]
         self.nslots = int(nslots)
-        self.partials = torch.zeros(max(self.nslots, 1) * 2, dtype=torch.float32, device=device)
+        self.partials = torch.zeros(max(self.nslots, 1) * 2, dtype=torch.float32,
+                                    device=self.device)
+
+    def halo_range(self, chunk: Optional[int] = None):
+        if chunk is None:
+            return 0, self.n
+        return self.chunk_halos[chunk], self.chunk_halos[chunk + 1]
 
     def fwd_blocks(self, nhalos: int, nbins: int = 10, log_sigma: bool = True) -> int:
         """Forward grid: enough 256-thread workgroups for the halos (4 per thread per
@@ -174,26 +197,74 @@ def _build_tiles(counts, breaks, tile_halos, tile_pops):
 
 
 # ---------------------------------------------------------------------------- device ops
+def smf_forward_slab(theta: torch.Tensor, shard: PopulationShard, bins: SmfBins, log_sigma: bool,
+                     slab: torch.Tensor, chunk: Optional[int] = None) -> int:
+    """Forward of the shard (or one population chunk) into per-workgroup slab rows;
+    returns the number of rows written.  CPU: one row from the PyTorch reference."""
+    h0, h1 = shard.halo_range(chunk)
+    if theta.device.type != "cuda":
+        with torch.no_grad():
+            xs = shard.x[h0:h1]
+            ps = None if shard.pop is None else shard.pop[h0:h1]
+            row = smf_sumstats_reference(theta.reshape(-1).float(), xs, ps, bins, log_sigma)
+            sc = torch.as_tensor(bins.scale, dtype=row.dtype)
+        slab[:bins.nbp].zero_()
+        slab[:bins.nb] = (row / sc).to(slab.dtype)  # unscaled bin sums (scale at reduce)
+        return 1
+    nblk = shard.fwd_blocks(max(h1 - h0, 1), bins.nb, log_sigma)
+    ext().smf_forward(shard.x, shard.pop, theta, list(bins.edges), list(bins.scale),
+                      bool(log_sigma), h0, h1, slab, nblk)
+    return nblk
+
+
+def smf_slab_reduce(slab: torch.Tensor, nrows: int, bins: SmfBins, out: torch.Tensor) -> torch.Tensor:
+    """Fixed-order sum of ``nrows`` slab rows per bin, times the bin scale -> ``out``."""
+    if slab.device.type != "cuda":
+        rows = slab[:nrows * bins.nbp].reshape(nrows, bins.nbp).double().sum(0)
+        sc = torch.zeros(bins.nbp, dtype=torch.float64)
+        sc[:bins.nb] = torch.as_tensor(bins.scale, dtype=torch.float64)
+        out[:bins.nbp] = (rows * sc).to(out.dtype)
+        return out
+    ext().smf_slab_reduce(slab, nrows, list(bins.edges), list(bins.scale), out)
+    return out
+
+
 def smf_forward_into(theta: torch.Tensor, shard: PopulationShard, bins: SmfBins, log_sigma: bool,
                      out: torch.Tensor, slab: Optional[torch.Tensor] = None,
                      chunk: Optional[int] = None) -> torch.Tensor:
     """Partial sumstats of the shard (or one population chunk) into ``out[:nbp]``."""
-    E = ext()
-    if chunk is None:
-        h0, h1 = 0, shard.n
-    else:
-        h0, h1 = shard.chunk_halos[chunk], shard.chunk_halos[chunk + 1]
-    nblk = shard.fwd_blocks(max(h1 - h0, 1), bins.nb, log_sigma)
     if slab is None:
+        h0, h1 = shard.halo_range(chunk)
+        nblk = shard.fwd_blocks(max(h1 - h0, 1), bins.nb, log_sigma)
         slab = torch.empty(nblk * bins.nbp, dtype=torch.float32, device=theta.device)
-    E.smf_forward(shard.x, shard.pop, theta, list(bins.edges), list(bins.scale), bool(log_sigma),
-                  h0, h1, slab, nblk)
-    E.smf_slab_reduce(slab, nblk, list(bins.edges), list(bins.scale), out)
-    return out
+    nrows = smf_forward_slab(theta, shard, bins, log_sigma, slab, chunk)
+    return smf_slab_reduce(slab, nrows, bins, out)
 
 
 def smf_vjp_into(theta: torch.Tensor, shard: PopulationShard, bins: SmfBins, log_sigma: bool,
                  h: torch.Tensor, grad: torch.Tensor, chunk: Optional[int] = None) -> torch.Tensor:
+    """Per-population VJP with edge weights ``h`` into ``grad`` (the chunk's parameters
+    only).  CPU: autograd of the PyTorch reference restricted to the chunk's halos."""
+    if theta.device.type != "cuda":
+        h0, h1 = shard.halo_range(chunk)
+        p0, p1 = (0, shard.npop) if chunk is None else (shard.chunk_pops[chunk], shard.chunk_pops[chunk + 1])
+        th = theta.detach().reshape(-1)[:2 * shard.npop].double().clone().requires_grad_(True)
+        xs = shard.x[h0:h1].double()
+        ps = None if shard.pop is None else shard.pop[h0:h1]
+        hw = h[:bins.nb + 1].double() * math.sqrt(2 * math.pi)
+        with torch.enable_grad():
+            t2 = th.reshape(-1, 2)
+            a = t2[:, 0][ps.long()] if ps is not None else t2[0, 0]
+            sg = t2[:, 1][ps.long()] if ps is not None else t2[0, 1]
+            sigma = torch.pow(torch.tensor(10.0, dtype=th.dtype), sg) if log_sigma else sg
+            e = torch.as_tensor(bins.edges, dtype=th.dtype)
+            z = (e[None, :] - (xs + a)[:, None]) / (sigma[:, None] if torch.is_tensor(sigma) and sigma.dim() else sigma)
+            f = (normal_cdf(z) * hw[None, :]).sum()
+            (g,) = torch.autograd.grad(f, th, allow_unused=True)
+        if g is None:
+            g = torch.zeros_like(th)
+        grad.reshape(-1)[2 * p0:2 * p1] = g[2 * p0:2 * p1].to(grad.dtype)
+        return grad
     E = ext()
     if chunk is None:
         t0, t1 = 0, shard.tiles.shape[0]
@@ -204,6 +275,20 @@ def smf_vjp_into(theta: torch.Tensor, shard: PopulationShard, bins: SmfBins, log
     E.smf_vjp(shard.x, shard.pop, theta, shard.tiles, t0, t1, h, list(bins.edges),
               list(bins.scale), bool(log_sigma), grad, shard.partials, shard.giant[g0:g1])
     return grad
+
+
+def smf_edge_weights_into(g: torch.Tensor, bins: SmfBins, h: torch.Tensor) -> torch.Tensor:
+    """h_e = (g_{e-1} scale_{e-1} - g_e scale_e) / sqrt(2 pi) for e in [0, nb]."""
+    if g.device.type != "cuda":
+        sc = torch.as_tensor(bins.scale, dtype=torch.float64)
+        gg = g[:bins.nb].double() * sc
+        hh = torch.zeros(bins.nbp + 1, dtype=torch.float64)
+        hh[1:bins.nb + 1] += gg
+        hh[:bins.nb] -= gg
+        h[:bins.nbp + 1] = (hh / math.sqrt(2 * math.pi)).to(h.dtype)
+        return h
+    ext().smf_edge_weights(g, list(bins.edges), list(bins.scale), h)
+    return h
 
 
 class _SmfSumstats(torch.autograd.Function):
@@ -221,7 +306,7 @@ class _SmfSumstats(torch.autograd.Function):
         bins = ctx.bins
         g = gS.detach().to(torch.float32).contiguous()
         h = torch.empty(bins.nbp + 1, dtype=torch.float32, device=theta.device)
-        ext().smf_edge_weights(g, list(bins.edges), list(bins.scale), h)
+        smf_edge_weights_into(g, bins, h)
         grad = torch.empty_like(theta, dtype=torch.float32)
         smf_vjp_into(theta.detach().contiguous(), ctx.shard, bins, ctx.log_sigma, h, grad)
         return grad.to(theta.dtype), None, None, None
