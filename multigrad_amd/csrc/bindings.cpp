@@ -28,6 +28,12 @@ void fused_adam(torch::Tensor u, torch::Tensor m, torch::Tensor v, torch::Tensor
                 c10::optional<torch::Tensor> hi, c10::optional<torch::Tensor> kind,
                 torch::Tensor step, double lr, double b1, double b2, double eps, bool legacy,
                 c10::optional<torch::Tensor> traj, int64_t traj_stride);
+// lbfgs.hip
+void multi_dot(torch::Tensor A, int64_t nrows, std::vector<torch::Tensor> B, int64_t n,
+               torch::Tensor out, torch::Tensor workspace);
+int64_t multi_dot_workspace(int64_t nrows, int64_t n);
+void lincomb(torch::Tensor H, int64_t nrows, torch::Tensor coef, double alpha,
+             c10::optional<torch::Tensor> x, int64_t n, torch::Tensor y);
 // runtime.cpp
 std::tuple<torch::Tensor, torch::Tensor, torch::Tensor, torch::Tensor, int64_t>
 build_tiles(torch::Tensor counts, std::vector<int64_t> breaks, int64_t tile_halos,
@@ -45,6 +51,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("smf_logmse", &mg::smf_logmse);
   m.def("smf_vjp", &mg::smf_vjp);
   m.def("fused_adam", &mg::fused_adam);
+  m.def("multi_dot", &mg::multi_dot);
+  m.def("multi_dot_workspace", &mg::multi_dot_workspace);
+  m.def("lincomb", &mg::lincomb);
   m.def("build_tiles", &mg::build_tiles);
   m.def("sort_by_population", &mg::sort_by_population);
 }

@@ -292,6 +292,13 @@ class FusedAdamEngine:
     def last_loss(self) -> float:
         return float(self.loss.item())
 
+    # ------------------------------------------------------------------ L-BFGS objective
+    def lbfgs_objective(self, guess):
+        """Objective over this rank's optimizer-owned parameters for
+        :func:`multigrad_amd.optim.lbfgs.lbfgs_minimize` (sharded under ZeRO)."""
+        self.setup(guess, nsteps=1, history="last")
+        return _EngineObjective(self)
+
     # ------------------------------------------------------------------ driver
     def run_adam(self, guess, nsteps: int = 100, param_bounds=None, learning_rate: float = 0.01,
                  b1: float = 0.9, b2: float = 0.999, eps: float = 1e-8, history="full",
@@ -305,3 +312,68 @@ class FusedAdamEngine:
                 callback(i, self.loss, self)
         self.drain()
         return self.history.result()
+
+
+class _EngineObjective:
+    """Loss and gradient over the engine's owned parameter slices.
+
+    ZeRO (world > 1): x is the concatenation of this rank's slices of every chunk; an
+    evaluation all-gathers the chunks, runs forward + loss + per-chunk VJP, and
+    reduce-scatters the gradient back to the owned slices -- L-BFGS vectors and history
+    are sharded 1/W and its dot products are all-reduced by the optimizer.
+    Replicated: x is the full (padded) parameter vector and the gradient is all-reduced.
+    """
+
+    def __init__(self, eng: FusedAdamEngine):
+        self.e = eng
+        self.comm = eng.comm
+        self.sharded = eng.zero
+        self.device = eng.device
+        self.n_local = sum(eng.loc_len) if eng.zero else eng.P_pad
+
+    def x0(self) -> torch.Tensor:
+        e = self.e
+        if not e.zero:
+            return e.theta.clone()
+        return torch.cat([e.theta[a:b] for a, b in e.own]).contiguous()
+
+    def _load(self, x: torch.Tensor):
+        e = self.e
+        if not e.zero:
+            e.theta.copy_(x)
+            return
+        for c in range(e.C):
+            a, b = e.own[c]
+            o, n = e.loc_off[c], e.loc_len[c]
+            e.theta[a:b].copy_(x[o:o + n])
+            pa, L = e.pb[c], e.lengths[c]
+            e._ag[c] = e.comm.all_gather_into_tensor(e.theta[pa:pa + L], e.theta[a:b], async_op=True)
+            e._ag_row[c] = None
+
+    def __call__(self, x: torch.Tensor):
+        e, md = self.e, self.e.model
+        self._load(x)
+        e._forward_loss()
+        if e.zero:
+            works = []
+            for c in range(e.C):
+                md.engine_vjp_into(e.theta, e.h, e.grad, chunk=c)
+                a, L = e.pb[c], e.lengths[c]
+                o, n = e.loc_off[c], e.loc_len[c]
+                works.append(e.comm.reduce_scatter_tensor(e.g_loc[o:o + n], e.grad[a:a + L],
+                                                          async_op=True))
+            for w in works:
+                w.wait()
+            g = e.g_loc
+        else:
+            for c in range(e.C):
+                md.engine_vjp_into(e.theta, e.h, e.grad, chunk=c if e.C > 1 else None)
+            if e.size > 1:
+                e.comm.all_reduce(e.grad)
+            g = e.grad
+        return float(e.loss.double().item()), g
+
+    def full(self, x: torch.Tensor) -> torch.Tensor:
+        self._load(x)
+        self.e.drain()
+        return self.e.theta[:self.e.P].clone()

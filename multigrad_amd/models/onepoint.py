@@ -95,12 +95,34 @@ class _OptimizerFrontEnds:
                               randkey=randkey, comm=comm, **kw)
 
     def run_bfgs(self, guess, maxsteps: int = 100, param_bounds=None, randkey=None,
-                 comm=None, **kw):
-        """L-BFGS-B (scipy on the root rank); returns an ``OptimizeResult`` on every rank."""
+                 comm=None, method: str = "auto", **kw):
+        """L-BFGS(-B); returns a ``scipy.optimize.OptimizeResult`` on every rank.
+
+        ``method="scipy"``: scipy's L-BFGS-B on the root rank, other ranks serve its
+        evaluations (the reference's protocol, exact box-constraint semantics).
+        ``method="device"``: SPMD device L-BFGS with all-reduced dot products (bounds via
+        the Adam transforms); models with the fused-engine protocol run it over the
+        ZeRO-sharded engine.  ``"auto"`` picks ``device`` above 1e5 parameters.
+        """
         comm = self._opt_comm() if comm is None else comm
-        return _bfgs.run_bfgs(self.calc_loss_and_grad_from_params, guess, maxsteps=maxsteps,
-                              param_bounds=param_bounds, randkey=randkey, comm=comm,
-                              device=self.param_device(), **kw)
+        x0 = as_param_tensor(guess, device=self.param_device())
+        if method == "auto":
+            method = "device" if x0.numel() > 100_000 else "scipy"
+        if method == "scipy":
+            return _bfgs.run_bfgs(self.calc_loss_and_grad_from_params, x0, maxsteps=maxsteps,
+                                  param_bounds=param_bounds, randkey=randkey, comm=comm,
+                                  device=self.param_device(), **kw)
+        from ..optim import lbfgs as _lbfgs
+        hist = kw.pop("history", 10)
+        fused = getattr(self, "fused_engine", None)
+        if fused is not None and param_bounds is None and randkey is None:
+            eng = fused(comm=comm, **{k: kw.pop(k) for k in ("zero", "chunks") if k in kw})
+            if eng is not None:
+                obj = eng.lbfgs_objective(x0)
+                return _lbfgs.lbfgs_minimize(obj, maxiter=maxsteps, m=hist, **kw)
+        return _lbfgs.run_lbfgs_device(self.calc_loss_and_grad_from_params, x0, maxsteps=maxsteps,
+                                       param_bounds=param_bounds, randkey=randkey, comm=comm,
+                                       history=hist, **kw)
 
 
 @dataclass

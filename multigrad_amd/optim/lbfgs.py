@@ -1,0 +1,282 @@
+"""Device L-BFGS with globally consistent (all-reduced) dot products.
+
+The reference's ``run_bfgs`` (``multigrad/bfgs.py:32-113``) runs scipy's compiled
+L-BFGS-B on the root rank and broadcasts every trial point.  For 1e6-1e8 parameters the
+optimizer itself must live on the GPUs, so this is an SPMD L-BFGS:
+
+* vectors (x, g, the m (s, y) history pairs) are device tensors -- replicated, or
+  **sharded 1/W per rank** when driven by the ZeRO engine (each rank owns a slice of
+  every vector, BASELINE config 4);
+* the inverse-Hessian product uses the compact representation (Byrd, Nocedal & Schnabel
+  1994), so one iteration needs the 2m x 3 inner products [S; Y] . [s_new, y_new, g_new]:
+  one fused pass (``csrc/lbfgs.hip: multi_dot``, fp64 deterministic reduction) and ONE
+  small all-reduce of 6m doubles -- instead of the two-loop recursion's 2m *sequential*
+  reductions;
+* the search direction ``d = -(gamma g + S a + gamma Y b)`` is one fused pass
+  (``lincomb``);
+* the strong-Wolfe line search (Nocedal & Wright Alg. 3.5/3.6, cubic interpolation)
+  decides on loss values and directional derivatives that are bitwise identical on all
+  ranks (all-reduced), so every rank takes the same decisions without broadcasts.
+
+Termination follows scipy's L-BFGS-B: ``(f_k - f_{k+1}) / max(|f_k|, |f_{k+1}|, 1) <= ftol``
+or ``max|g| <= gtol`` or ``maxiter``.  Box bounds are supported through the same
+bijective transforms as Adam (:mod:`multigrad_amd.optim.transforms`); the exact scipy
+L-BFGS-B projection semantics remain available through :func:`multigrad_amd.optim.bfgs.run_bfgs`.
+"""
+from __future__ import annotations
+
+import math
+from typing import Callable, Optional
+
+import numpy as np
+import scipy.linalg
+import scipy.optimize
+import torch
+
+from ..ops.lbfgs import MultiDot, lincomb_
+
+__all__ = ["lbfgs_minimize", "GenericObjective", "run_lbfgs_device"]
+
+_EPS = np.finfo(np.float64).eps
+
+
+class GenericObjective:
+    """Replicated objective around ``loss_and_grad_fn(x_full) -> (loss, grad)`` (the
+    gradient is already all-reduced by the model, so every rank holds the same vector)."""
+
+    def __init__(self, loss_and_grad_fn: Callable, x0: torch.Tensor, comm=None, bounds=None,
+                 **fn_kwargs):
+        self.fn = loss_and_grad_fn
+        self.kw = fn_kwargs
+        self.comm = comm
+        self.sharded = False
+        self.bounds = bounds
+        x0 = x0.detach().reshape(-1).to(torch.float32)
+        self.device = x0.device
+        self.shape = x0.shape
+        self.u0 = bounds.forward(x0) if bounds is not None else x0.clone()
+        self.n_local = self.u0.numel()
+
+    def x0(self) -> torch.Tensor:
+        return self.u0.clone()
+
+    def full(self, u: torch.Tensor) -> torch.Tensor:
+        return self.bounds.inverse(u) if self.bounds is not None else u
+
+    def __call__(self, u: torch.Tensor):
+        x = self.full(u)
+        loss, grad = self.fn(x, **self.kw)
+        if isinstance(loss, (tuple, list)):
+            loss = loss[0]
+        g = torch.as_tensor(grad).detach().reshape(-1).to(device=u.device, dtype=torch.float32)
+        if self.bounds is not None:
+            g = g * self.bounds.dpdu(u)
+        return float(torch.as_tensor(loss).detach().double()), g.contiguous()
+
+
+def _allreduce_np(comm, arr: np.ndarray, op="sum", sharded=True) -> np.ndarray:
+    if comm is None or comm.size == 1 or not sharded:
+        return arr
+    t = torch.from_numpy(np.ascontiguousarray(arr, dtype=np.float64))
+    comm.all_reduce(t, op=op)
+    return t.numpy()
+
+
+def _cubic_min(a, fa, da, b, fb, db):
+    """Minimiser of the cubic interpolating (a, fa, da), (b, fb, db) (None if degenerate)."""
+    d1 = da + db - 3 * (fa - fb) / (a - b)
+    disc = d1 * d1 - da * db
+    if disc < 0 or not np.isfinite(disc):
+        return None
+    d2 = math.copysign(math.sqrt(disc), b - a)
+    den = db - da + 2 * d2
+    if den == 0:
+        return None
+    return b - (b - a) * (db + d2 - d1) / den
+
+
+def lbfgs_minimize(obj, maxiter: int = 100, m: int = 10, ftol: float = 1e7 * _EPS,
+                   gtol: float = 1e-5, maxls: int = 20, c1: float = 1e-4, c2: float = 0.9,
+                   callback=None) -> scipy.optimize.OptimizeResult:
+    """Minimise ``obj`` (see :class:`GenericObjective`) with L-BFGS; SPMD-consistent."""
+    comm, sharded = obj.comm, obj.sharded
+    n = obj.n_local
+    dev = obj.device
+    x = obj.x0().contiguous()
+    f, g = obj(x)
+    g = g.clone()
+    nfev = 1
+    HS = torch.zeros((2 * m, n), dtype=torch.float32, device=dev)  # rows: S slots, Y slots
+    dot = MultiDot(2 * m, n, dev)
+    dot1 = MultiDot(1, n, dev)
+    SY = np.zeros((m, m))
+    YY = np.zeros((m, m))
+    Sg = np.zeros(m)
+    Yg = np.zeros(m)
+    order: list = []  # ring slots, oldest -> newest
+    d = torch.empty_like(x)
+    xt = torch.empty_like(x)
+    coef = torch.zeros(2 * m, dtype=torch.float32, device=dev)
+
+    def gdot(a: torch.Tensor, b: torch.Tensor) -> float:
+        v = dot1(a.view(1, -1), 1, [b]).cpu().numpy().reshape(-1)
+        return float(_allreduce_np(comm, v, sharded=sharded)[0])
+
+    def ginf(v: torch.Tensor) -> float:
+        loc = np.array([float(v.abs().max()) if v.numel() else 0.0])
+        return float(_allreduce_np(comm, loc, op="max", sharded=sharded)[0])
+
+    status, message = 1, "STOP: TOTAL NO. of ITERATIONS REACHED LIMIT"
+    nit = 0
+    if ginf(g) <= gtol:
+        status, message = 0, "CONVERGENCE: NORM_OF_PROJECTED_GRADIENT_<=_PGTOL"
+    else:
+        for k in range(maxiter):
+            # ---------------- search direction (compact inverse-Hessian product)
+            if order:
+                idx = np.array(order)
+                gamma, a, b = compact_coefficients(SY, YY, Sg, Yg, order)
+                cvec = np.zeros(2 * m)
+                cvec[idx] = -a
+                cvec[m + idx] = -gamma * b
+                coef.copy_(torch.from_numpy(cvec.astype(np.float32)))
+                lincomb_(HS, 2 * m, coef, -gamma, g, d)
+            else:
+                d.copy_(-g)
+            gd = gdot(g, d)
+            if not np.isfinite(gd) or gd >= 0:  # not a descent direction: reset memory
+                order.clear()
+                d.copy_(-g)
+                gd = gdot(g, d)
+            a1 = 1.0 if order else min(1.0, 1.0 / math.sqrt(max(-gd, 1e-300)))
+            # ---------------- strong-Wolfe line search
+            cache = {}
+
+            def phi(alpha):
+                nonlocal nfev
+                lincomb_(d.view(1, -1), 1, torch.tensor([alpha], dtype=torch.float32, device=dev),
+                         1.0, x, xt)
+                fa, ga = obj(xt)
+                nfev += 1
+                ga = ga.clone()
+                da = gdot(ga, d)
+                cache[alpha] = (fa, ga, da)
+                return fa, da
+
+            f0, d0 = f, gd
+            a_prev, f_prev, dphi_prev = 0.0, f0, d0
+            alpha, best = a1, None
+            for i in range(maxls):
+                fa, da = phi(alpha)
+                if not np.isfinite(fa) or fa > f0 + c1 * alpha * d0 or (i > 0 and fa >= f_prev):
+                    best = _zoom(phi, a_prev, alpha, f_prev, fa, dphi_prev, da, f0, d0, c1, c2, maxls)
+                    break
+                if abs(da) <= -c2 * d0:
+                    best = alpha
+                    break
+                if da >= 0:
+                    best = _zoom(phi, alpha, a_prev, fa, f_prev, da, dphi_prev, f0, d0, c1, c2, maxls)
+                    break
+                a_prev, f_prev, dphi_prev = alpha, fa, da
+                alpha = alpha * 2.0
+            if best is None or best not in cache:
+                # no acceptable step: keep the best decrease seen, else stop
+                cands = [(v[0], a) for a, v in cache.items() if v[0] < f0]
+                if not cands:
+                    status, message = 2, "ABNORMAL_TERMINATION_IN_LNSRCH"
+                    break
+                best = min(cands)[1]
+            f_new, g_new, _ = cache[best]
+            # ---------------- update iterate and history
+            s_vec = d * best
+            x.add_(s_vec)
+            y_vec = g_new - g
+            nit = k + 1
+            sy_new = gdot(s_vec, y_vec)
+            yy_new = gdot(y_vec, y_vec)
+            inserted = sy_new > _EPS * yy_new and yy_new > 0
+            if inserted:
+                q = order.pop(0) if len(order) == m else min(set(range(m)) - set(order))
+                HS[q].copy_(s_vec)
+                HS[m + q].copy_(y_vec)
+                order.append(q)
+                dots = dot(HS, 2 * m, [HS[q], HS[m + q], g_new]).cpu().numpy()
+            else:
+                dots = dot(HS, 2 * m, [g_new]).cpu().numpy()
+            dots = _allreduce_np(comm, dots, sharded=sharded)
+            if inserted:
+                for o in order:
+                    SY[o, q] = dots[o, 1]          # s_o . y_q
+                    SY[q, o] = dots[m + o, 0]      # s_q . y_o
+                    YY[o, q] = YY[q, o] = dots[m + o, 1]
+                Sg[:] = dots[:m, 2]
+                Yg[:] = dots[m:, 2]
+            else:
+                Sg[:] = dots[:m, 0]
+                Yg[:] = dots[m:, 0]
+            f_old, f, g = f, f_new, g_new
+            if callback is not None:
+                callback(obj.full(x))
+            if ginf(g) <= gtol:
+                status, message = 0, "CONVERGENCE: NORM_OF_PROJECTED_GRADIENT_<=_PGTOL"
+                break
+            if (f_old - f) <= ftol * max(abs(f_old), abs(f), 1.0):
+                status, message = 0, "CONVERGENCE: REL_REDUCTION_OF_F_<=_FACTR*EPSMCH"
+                break
+    xf = obj.full(x)
+    if getattr(obj, "finalize", None) is not None:
+        xf = obj.finalize(x)
+    return scipy.optimize.OptimizeResult(
+        x=xf, fun=f, jac=g, nit=nit, nfev=nfev, njev=nfev, status=status,
+        success=status == 0, message=message)
+
+
+def compact_coefficients(SY, YY, Sg, Yg, order):
+    """Coefficients of the compact L-BFGS product ``H g = gamma g + S a + gamma Y b``
+    (Byrd, Nocedal & Schnabel 1994) from the inner products of the pairs listed in
+    ``order`` (oldest first): returns ``(gamma, a, b)``."""
+    idx = np.asarray(order)
+    sy = SY[np.ix_(idx, idx)]
+    yy = YY[np.ix_(idx, idx)]
+    last = order[-1]
+    gamma = SY[last, last] / YY[last, last]
+    R = np.triu(sy)
+    D = np.diag(np.diag(sy))
+    t = scipy.linalg.solve_triangular(R, Sg[idx], lower=False)
+    a = scipy.linalg.solve_triangular(R, (D + gamma * yy) @ t - gamma * Yg[idx], lower=False,
+                                      trans="T")
+    return gamma, a, -t
+
+
+def _zoom(phi, lo, hi, flo, fhi, dlo, dhi, f0, d0, c1, c2, maxiter):
+    for _ in range(maxiter):
+        a = _cubic_min(lo, flo, dlo, hi, fhi, dhi)
+        span = hi - lo
+        lo_b, hi_b = min(lo, hi) + 0.1 * abs(span), max(lo, hi) - 0.1 * abs(span)
+        if a is None or not (lo_b <= a <= hi_b):
+            a = 0.5 * (lo + hi)
+        fa, da = phi(a)
+        if not np.isfinite(fa) or fa > f0 + c1 * a * d0 or fa >= flo:
+            hi, fhi, dhi = a, fa, da
+        else:
+            if abs(da) <= -c2 * d0:
+                return a
+            if da * (hi - lo) >= 0:
+                hi, fhi, dhi = lo, flo, dlo
+            lo, flo, dlo = a, fa, da
+        if abs(hi - lo) < 1e-12 * max(1.0, abs(lo)):
+            break
+    return lo if lo != 0.0 else None
+
+
+def run_lbfgs_device(loss_and_grad_fn: Callable, params, maxsteps: int = 100, param_bounds=None,
+                     randkey=None, comm=None, history: int = 10, **kw):
+    """Device L-BFGS for a generic ``loss_and_grad_fn(params[, randkey])`` (replicated)."""
+    from ..utils.random import init_randkey
+    from .transforms import Bounds
+    from ..utils.tensors import as_param_tensor
+    x0 = as_param_tensor(params)
+    bounds = Bounds.from_spec(param_bounds, x0.numel(), device=x0.device, dtype=torch.float32)
+    fkw = {} if randkey is None else {"randkey": init_randkey(randkey)}
+    obj = GenericObjective(loss_and_grad_fn, x0, comm=comm, bounds=bounds, **fkw)
+    return lbfgs_minimize(obj, maxiter=maxsteps, m=history, **kw)
