@@ -210,6 +210,7 @@ def test_device_lbfgs_population_engine():
     res = model.run_bfgs(data["guess"], maxsteps=40, method="device")
     assert res.x.is_cuda and res.x.shape == (2000,)
     assert res.fun < 1e-3 * f0
-    # same objective through the generic (autograd) path reaches a comparable loss
-    res2 = model.run_bfgs(data["guess"], maxsteps=40, method="device", randkey=None, history=10,
-                          gtol=1e-5) if False else None
+    # the generic (autograd + replicated-vector) device L-BFGS reaches a comparable loss
+    from multigrad_amd.optim.lbfgs import run_lbfgs_device
+    res2 = run_lbfgs_device(model.calc_loss_and_grad_from_params, data["guess"], maxsteps=40)
+    assert res2.fun < 1e-3 * f0
