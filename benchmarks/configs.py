@@ -1,0 +1,115 @@
+"""BASELINE.json configurations 1-5 (one JSON line each).
+
+  1  toy      -- sum-of-squares, 10 params, single-process Adam on CPU
+  2  adam1e6  -- population SMF model, 1e6 params, Adam, this node's ranks (1 GPU: config 2)
+  3            (same as 2 launched on 8 ranks: config 3)
+  4  lbfgs    -- device L-BFGS with all-reduced dot products (ZeRO-sharded on >1 rank)
+  5  adam1e8  -- 1e8-param model, fused Adam (history="last": a full 1e8 x steps trajectory
+               would not be a meaningful benchmark)
+
+    python benchmarks/configs.py --which toy adam1e6 lbfgs
+    python -m multigrad_amd.launch -n 8 benchmarks/configs.py --which adam1e6 lbfgs adam1e8
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+os.environ.setdefault("MULTIGRAD_PROGRESS", "0")
+
+
+def _sync():
+    import torch
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+
+
+def toy(comm, steps):
+    import torch
+    from multigrad_amd.models.toy import SumOfSquaresModel, make_toy_data
+    from multigrad_amd.parallel.comm import SerialComm
+    m = SumOfSquaresModel(aux_data=make_toy_data(ndim=10, npoints=1000, comm=SerialComm()),
+                          comm=SerialComm())
+    m.run_adam(torch.zeros(10), nsteps=5, learning_rate=0.05)
+    t0 = time.perf_counter()
+    traj = m.run_adam(torch.zeros(10), nsteps=steps, learning_rate=0.05)
+    dt = time.perf_counter() - t0
+    return {"config": "toy-10param-adam-cpu", "value": steps / dt, "unit": "steps/s",
+            "n_ranks": 1, "final_dist_to_mean": float((traj[-1] - torch.as_tensor(m.aux_data["mean"])).abs().max())}
+
+
+def adam(comm, steps, params, halos, history):
+    import torch
+    from multigrad_amd.models.population import PopulationSMFModel, make_population_data
+    dev = torch.device("cuda", torch.cuda.current_device())
+    data = make_population_data(params, halos, seed=1234, comm=comm, device=dev)
+    m = PopulationSMFModel(aux_data=data, comm=comm)
+    m.set_target_from_truth()
+    eng = m.fused_engine()
+    eng.setup(data["guess"], nsteps=steps + 3, learning_rate=1e-3, history=history)
+    for _ in range(3):
+        eng.step()
+    _sync(); comm.barrier(); _sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        eng.step()
+    _sync(); comm.barrier()
+    dt = time.perf_counter() - t0
+    return {"config": f"adam-{params:.0e}param", "value": steps / dt, "unit": "steps/s",
+            "n_ranks": comm.size, "halos": halos, "zero": eng.zero, "chunks": eng.C,
+            "loss": eng.last_loss()}
+
+
+def lbfgs(comm, iters, params, halos):
+    import torch
+    from multigrad_amd.models.population import PopulationSMFModel, make_population_data
+    from multigrad_amd.optim.lbfgs import lbfgs_minimize
+    dev = torch.device("cuda", torch.cuda.current_device())
+    data = make_population_data(params, halos, seed=1234, comm=comm, device=dev)
+    m = PopulationSMFModel(aux_data=data, comm=comm)
+    m.set_target_from_truth()
+    obj = m.fused_engine().lbfgs_objective(data["guess"])
+    _sync(); comm.barrier()
+    t0 = time.perf_counter()
+    res = lbfgs_minimize(obj, maxiter=iters, gtol=0.0, ftol=0.0)
+    _sync(); comm.barrier()
+    dt = time.perf_counter() - t0
+    return {"config": f"lbfgs-{params:.0e}param", "value": res.nit / dt, "unit": "iterations/s",
+            "fevals_per_s": res.nfev / dt, "n_ranks": comm.size, "nit": int(res.nit),
+            "nfev": int(res.nfev), "fun": float(res.fun), "sharded": bool(obj.sharded)}
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--which", nargs="+", default=["toy", "adam1e6", "lbfgs"])
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--halos", type=int, default=1 << 27)
+    args = ap.parse_args(argv)
+    import torch
+    import multigrad_amd as mg
+    comm = mg.init_distributed() if int(os.environ.get("WORLD_SIZE", "1")) > 1 else mg.get_world_comm()
+    if torch.cuda.is_available():
+        torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")) % torch.cuda.device_count())
+    out = []
+    for w in args.which:
+        if w == "toy":
+            r = toy(comm, 200) if comm.rank == 0 else None
+        elif w == "adam1e6":
+            r = adam(comm, args.steps, 1_000_000, args.halos, "full")
+        elif w == "adam1e7":
+            r = adam(comm, args.steps, 10_000_000, args.halos, "full")
+        elif w == "adam1e8":
+            r = adam(comm, args.steps, 100_000_000, args.halos * 4, "last")
+        elif w == "lbfgs":
+            r = lbfgs(comm, 20, 10_000_000, args.halos)
+        else:
+            raise SystemExit(f"unknown config {w}")
+        if comm.rank == 0 and r is not None:
+            print(json.dumps(r), flush=True)
+            out.append(r)
+
+
+if __name__ == "__main__":
+    main()

@@ -10,6 +10,7 @@ from .models.onepoint import OnePointModel, OnePointGroup
 from .parallel.subcomm import reduce_sum, split_subcomms, split_subcomms_by_node
 from .parallel.comm import get_world_comm, init_distributed
 from .utils import util
+from . import parallel
 from .optim import adam, bfgs
 
 __all__ = ["OnePointModel", "OnePointGroup", "reduce_sum", "split_subcomms",
