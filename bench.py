@@ -8,9 +8,12 @@ fixed, each of N ranks owns 1/N of it), random-init truth parameters.
 
 Every timed step does the full work of the reference's Adam step
 (multigrad/adam.py:59-66 + multigrad/multigrad.py:508-538): forward over all local
-halos, all-reduce of the sumstats, loss + cotangent, VJP over all local halos,
-all-reduce of the 1e7-float gradient, Adam update of all 1e7 parameters, and the
-trajectory write of the new parameters.
+halos, all-reduce of the sumstats, loss + cotangent, VJP over all local halos, the
+cross-rank sum of the dense 1e7-float gradient, the Adam update of all 1e7 parameters,
+and the trajectory write of the new parameters.  On one GPU the step is a replayed HIP
+graph; on N GPUs the gradient sum is a chunked RCCL reduce-scatter (overlapped with the
+VJP), Adam runs on each rank's 1/N slice, and the parameters come back with an in-place
+all-gather (ZeRO-1) -- the same bytes as one all-reduce.
 
 Usage: ``python bench.py [--gpus N] [--steps K] [--warmup W]``; for N>1 launch with
 ``python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py``.
@@ -73,6 +76,7 @@ def main(argv=None):
     t0 = time.perf_counter()
     for _ in range(args.steps):
         engine.step()
+    engine.drain()  # last all-gathers joined into the compute stream
     torch.cuda.synchronize()
     comm.barrier()
     elapsed = time.perf_counter() - t0
@@ -107,6 +111,8 @@ def main(argv=None):
             "optimizer": "Adam (fused HIP kernel), full trajectory" if history == "full"
                          else f"Adam (fused HIP kernel), history={history}",
             "graph": bool(engine.use_graph),
+            "optimizer_sharding": "zero1" if engine.zero else "replicated",
+            "chunks": engine.C,
         },
         "loss_first_timed": loss0,
         "loss_last": loss1,

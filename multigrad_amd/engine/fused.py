@@ -85,7 +85,13 @@ class FusedAdamEngine:
     zero : shard the optimizer across ranks (reduce-scatter / all-gather); default on
         for more than one rank (``MULTIGRAD_ZERO``)
     chunks : number of parameter chunks for collective/compute overlap (default 1 on a
-        single rank, 8 otherwise; ``MULTIGRAD_CHUNKS``)
+        single rank, 4 otherwise; ``MULTIGRAD_CHUNKS``)
+
+    With ZeRO the parameter all-gathers run on a second communicator (its own RCCL
+    stream), so the all-gather of chunk c overlaps the reduce-scatter of chunk c+1
+    instead of queueing behind it; the trajectory is stored sharded (each rank records
+    the slices it owns, written by the Adam kernel) and assembled by one all-gather when
+    it is requested -- the analogue of the reference's end-of-run trajectory broadcast.
     """
 
     def __init__(self, model, comm=None, graph: Optional[bool] = None,
@@ -97,7 +103,8 @@ class FusedAdamEngine:
         z = _env_flag("MULTIGRAD_ZERO", zero)
         self.zero = (self.size > 1) if z is None else bool(z) and self.size > 1
         nc = chunks if chunks is not None else int(os.environ.get("MULTIGRAD_CHUNKS", "0")) or None
-        self.nchunks_req = nc if nc is not None else (1 if self.size == 1 else 8)
+        self.nchunks_req = nc if nc is not None else (1 if self.size == 1 else 4)
+        self.comm_ag = None  # second communicator (own RCCL stream) for parameter all-gathers
         g = _env_flag("MULTIGRAD_GRAPH", graph)
         self.use_graph = (self.size == 1) if g is None else bool(g)
         self.graph = None
@@ -169,9 +176,20 @@ class FusedAdamEngine:
             self.v = torch.zeros(P_pad, **f32)
         self.step_host = 0
         self.nsteps = int(nsteps)
-        self.history = History(history, nsteps, theta[:P].detach().clone())
+        self.history = History(history if not (self.zero and history == "full") else "last",
+                               nsteps, theta[:P].detach().clone())
+        self.traj_loc = None
+        self.history_mode = history
+        if self.zero:
+            if history == "full":
+                self.traj_loc = torch.zeros((self.nsteps + 1, sum(self.loc_len)), **f32)
+                for c in range(self.C):
+                    a, b = self.own[c]
+                    o, n = self.loc_off[c], self.loc_len[c]
+                    self.traj_loc[0, o:o + n] = theta[a:b]
+            if self.comm_ag is None and self.size > 1 and _env_flag("MULTIGRAD_AG_COMM", True):
+                self.comm_ag = self.comm.split(0)
         self._ag: List = [None] * self.C
-        self._ag_row = [None] * self.C
         self.graph = None
         self.ready = True
         return self
@@ -185,17 +203,12 @@ class FusedAdamEngine:
         return Bounds(b.lo[o:o + n], b.hi[o:o + n], b.kind[o:o + n])
 
     def _drain(self, c):
-        """Wait for chunk c's parameter all-gather and record its trajectory slice."""
+        """Wait for chunk c's parameter all-gather (stream-ordered)."""
         w = self._ag[c]
         if w is None:
             return
         w.wait()
         self._ag[c] = None
-        row = self._ag_row[c]
-        if row is not None and self.history.mode == "full":
-            a, b = self.pb[c], min(self.pb[c] + self.lengths[c], self.P)
-            if b > a:
-                self.history.buf[row, a:b].copy_(self.theta[a:b])
 
     def drain(self):
         for c in range(self.C):
@@ -232,13 +245,15 @@ class FusedAdamEngine:
                 o, n = self.loc_off[c], self.loc_len[c]
                 u = self.u_loc[o:o + n] if self.u_loc is not None else self.theta[a:b]
                 p = self.theta[a:b] if self.u_loc is not None else None
+                tb = None if self.traj_loc is None else self.traj_loc.reshape(-1)[o:]
                 adam_step_(u, self.m[o:o + n], self.v[o:o + n], self.g_loc[o:o + n], p,
                            self.step_dev[c], self.lr, self.b1, self.b2, self.eps,
-                           self._bslice(c), self.legacy)
+                           self._bslice(c), self.legacy, traj_base=tb,
+                           traj_stride=self.traj_loc.shape[1] if tb is not None else 0)
                 pa, L = self.pb[c], self.lengths[c]
-                self._ag[c] = self.comm.all_gather_into_tensor(self.theta[pa:pa + L],
-                                                               self.theta[a:b], async_op=True)
-                self._ag_row[c] = self.step_host + 1
+                agc = self.comm_ag if self.comm_ag is not None else self.comm
+                self._ag[c] = agc.all_gather_into_tensor(self.theta[pa:pa + L], self.theta[a:b],
+                                                         async_op=True)
         else:
             for c in range(self.C):
                 md.engine_vjp_into(self.theta, self.h, self.grad, chunk=c if self.C > 1 else None)
@@ -281,9 +296,28 @@ class FusedAdamEngine:
         else:
             self._enqueue_step()
         self.step_host += 1
-        if self.history.mode != "full":
+        if self.history.mode != "full" and self.traj_loc is None:
             self.drain()
             self.history.record(self.step_host - 1, self.theta[:self.P])
+
+    def trajectory(self) -> torch.Tensor:
+        """The recorded parameter trajectory (assembled across ranks under ZeRO)."""
+        self.drain()
+        if self.traj_loc is None:
+            return self.history.result()
+        W = self.size
+        nloc = self.traj_loc.shape[1]
+        rows = self.step_host + 1
+        gathered = torch.empty((W, rows, nloc), dtype=self.traj_loc.dtype, device=self.device)
+        self.comm.all_gather_into_tensor(gathered.reshape(-1),
+                                         self.traj_loc[:rows].contiguous().reshape(-1))
+        out = torch.empty((rows, self.P_pad), dtype=self.traj_loc.dtype, device=self.device)
+        for c in range(self.C):
+            o, n = self.loc_off[c], self.loc_len[c]
+            for r in range(W):
+                a = self.pb[c] + r * n
+                out[:, a:a + n] = gathered[r, :, o:o + n]
+        return out[:, :self.P]
 
     def params(self) -> torch.Tensor:
         self.drain()
@@ -310,8 +344,7 @@ class FusedAdamEngine:
             self.step()
             if callback is not None:
                 callback(i, self.loss, self)
-        self.drain()
-        return self.history.result()
+        return self.trajectory()
 
 
 class _EngineObjective:
@@ -347,8 +380,8 @@ class _EngineObjective:
             o, n = e.loc_off[c], e.loc_len[c]
             e.theta[a:b].copy_(x[o:o + n])
             pa, L = e.pb[c], e.lengths[c]
-            e._ag[c] = e.comm.all_gather_into_tensor(e.theta[pa:pa + L], e.theta[a:b], async_op=True)
-            e._ag_row[c] = None
+            agc = e.comm_ag if e.comm_ag is not None else e.comm
+            e._ag[c] = agc.all_gather_into_tensor(e.theta[pa:pa + L], e.theta[a:b], async_op=True)
 
     def __call__(self, x: torch.Tensor):
         e, md = self.e, self.e.model
