@@ -7,10 +7,10 @@
 namespace mg {
 // smf.hip
 int smf_padded_bins(int64_t nb);
-int64_t smf_fwd_max_blocks(int64_t nb, bool log_sigma, bool has_pop);
+int64_t smf_fwd_max_blocks(int64_t nb, bool log_sigma, bool has_pop, bool rel_tail);
 void smf_forward(torch::Tensor x, c10::optional<torch::Tensor> pop, torch::Tensor theta,
                  std::vector<double> edges, std::vector<double> scale, bool log_sigma,
-                 int64_t begin, int64_t end, torch::Tensor slab, int64_t nblocks);
+                 int64_t begin, int64_t end, torch::Tensor slab, int64_t nblocks, bool rel_tail);
 void smf_slab_reduce(torch::Tensor slab, int64_t nrows, std::vector<double> edges,
                      std::vector<double> scale, torch::Tensor out);
 void smf_edge_weights(torch::Tensor g, std::vector<double> edges, std::vector<double> scale,

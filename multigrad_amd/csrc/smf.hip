@@ -6,7 +6,8 @@
 //   mu_i = x_i + a_c ;  sigma_c = LOGSIG ? 10^{s_c} : s_c
 //   S_k  = scale_k * sum_i [ Phi((e_{k+1}-mu_i)/sigma) - Phi((e_k-mu_i)/sigma) ]
 // The reference issues one XLA dispatch per bin with 2 erf per halo per bin; here ONE
-// pass evaluates all NB+1 edge tails per halo (tail-accurate Q(z), see common.h), keeps
+// pass evaluates all NB+1 edge tails per halo (Q(z) to float32-erf absolute accuracy, or
+// tail-accurate to ~1e-6 relative: SmfBins.tail, see common.h), keeps
 // the NB bin sums in registers across a grid-stride loop, and reduces them
 // deterministically (wave shuffles -> LDS -> per-block slab -> fixed-order slab sum).
 //
@@ -29,6 +30,12 @@
 
 namespace mg {
 
+#ifndef MG_FWD_BALLOT
+#define MG_FWD_BALLOT 1  // integer counts per wave (SALU) instead of per lane (VALU)
+#endif
+#ifndef MG_VJP_EXP
+#define MG_VJP_EXP 0
+#endif
 constexpr int kMaxBins = 32;
 constexpr int kThreads = 256;
 constexpr int kItems = 8;                       // halos per thread in a tile
@@ -59,24 +66,28 @@ __device__ __forceinline__ float inv_sigma(float s) {
 // Work with the negated scaled coordinate n_e = -w_e = (mu - e_e) * kWScale / sigma.
 // With signed tails V_e = copysign(Q(|z_e|), n_e) and pos_e = [n_e < 0] = [z_e > 0]
 // (sign bit of n), Phi(z_e) = pos_e + V_e, so mass_k = (V_{k+1} - V_k) + (pos_{k+1} -
-// pos_k): the float part never cancels (tail differences) and the 0/1 part is
-// accumulated exactly as per-edge integer counts, folded in once per thread at the end.
-// A halo with x = -inf contributes exactly zero (used to mask the unrolled tail).
-template <int NB, bool LOGSIG>
-__device__ __forceinline__ void halo_mass(float x, float2 th, const SmfBins& b, float (&acc)[NB],
-                                          int (&cnt)[NB + 1]) {
+// pos_k).  Per thread the kernel accumulates the per-EDGE sums sum V_e (one fma per edge:
+// the sign is folded into the Gaussian factor) and the 0/1 parts as exact integer
+// counts; the per-bin differences are formed once per thread at the end.
+// A halo with x = -inf contributes exactly zero (used to mask the unrolled tail): every
+// V_e is -0 and every pos_e is 1, which cancels in the differences.
+template <int NB, bool LOGSIG, bool REL>
+__device__ __forceinline__ void halo_mass(float x, float2 th, const SmfBins& b,
+                                          float (&acc)[NB + 1], int (&cnt)[NB + 1]) {
   const float ninv = -inv_sigma<LOGSIG>(th.y) * kWScale;
   const float mu = -(x + th.x) * ninv;  // = (x + a) * kWScale / sigma
-  float np = fmaf(b.edge[0], ninv, mu);
-  float vp = __builtin_copysignf(normal_tail_w(np), np);
-  cnt[0] += (int)(__float_as_uint(np) >> 31);
 #pragma unroll
-  for (int k = 0; k < NB; ++k) {
-    const float n = fmaf(b.edge[k + 1], ninv, mu);
-    const float v = __builtin_copysignf(normal_tail_w(n), n);
-    cnt[k + 1] += (int)(__float_as_uint(n) >> 31);
-    acc[k] += v - vp;
-    vp = v;
+  for (int e = 0; e <= NB; ++e) {
+    const float n = fmaf(b.edge[e], ninv, mu);
+    float p, g;
+    normal_tail_parts_w<REL>(n, p, g);
+    acc[e] = fmaf(p, __builtin_copysignf(g, n), acc[e]);
+#if MG_FWD_BALLOT
+    // wave-wide count of the 0/1 parts: one v_cmp, the popcount/add run on the SALU
+    cnt[e] += __builtin_popcountll(__builtin_amdgcn_ballot_w64(n < 0.0f));
+#else
+    cnt[e] += (int)(__float_as_uint(n) >> 31);
+#endif
   }
 }
 
@@ -89,28 +100,32 @@ __device__ __forceinline__ void halo_mass(float x, float2 th, const SmfBins& b, 
 #endif
 constexpr int kFwdUnroll = MG_FWD_UNROLL;
 
-template <int NB, bool LOGSIG, bool HAS_POP>
+template <int NB, bool LOGSIG, bool HAS_POP, bool REL>
 __global__ __launch_bounds__(kThreads, MG_FWD_MINWAVES) void smf_fwd_kernel(
     const float* __restrict__ x, const int32_t* __restrict__ pop,
     const float2* __restrict__ theta, int64_t begin, int64_t end, SmfBins bins,
     float* __restrict__ slab) {
-  float acc[NB];
+  float acc[NB + 1];
   int cnt[NB + 1];
 #pragma unroll
-  for (int k = 0; k < NB; ++k) acc[k] = 0.0f;
+  for (int k = 0; k <= NB; ++k) acc[k] = 0.0f;
 #pragma unroll
   for (int k = 0; k <= NB; ++k) cnt[k] = 0;
   const float2 th0 = HAS_POP ? make_float2(0.f, 0.f) : theta[0];
   const int64_t stride = (int64_t)gridDim.x * kThreads;
-  for (int64_t i0 = begin + (int64_t)blockIdx.x * kThreads + threadIdx.x; i0 < end;
-       i0 += kFwdUnroll * stride) {
+  // the loop is wave-uniform (trip count from the wave's first halo; lanes past the end
+  // are masked with x = -inf), so the ballot counts stay in SGPRs and are complete
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wbase = __builtin_amdgcn_readfirstlane(threadIdx.x - lane);
+  for (int64_t w0 = begin + (int64_t)blockIdx.x * kThreads + wbase; w0 < end;
+       w0 += kFwdUnroll * stride) {
     // issue every load of this iteration before any math (one dependent round trip)
     float xs[kFwdUnroll];
     int ps[kFwdUnroll];
     float2 ths[kFwdUnroll];
 #pragma unroll
     for (int u = 0; u < kFwdUnroll; ++u) {
-      const int64_t i = i0 + u * stride;
+      const int64_t i = w0 + lane + u * stride;
       const bool ok = i < end;
       xs[u] = ok ? x[i] : -INFINITY;  // -inf: exactly zero contribution, no branch
       ps[u] = (HAS_POP && ok) ? pop[i] : 0;
@@ -118,12 +133,19 @@ __global__ __launch_bounds__(kThreads, MG_FWD_MINWAVES) void smf_fwd_kernel(
 #pragma unroll
     for (int u = 0; u < kFwdUnroll; ++u) ths[u] = HAS_POP ? theta[ps[u]] : th0;
 #pragma unroll
-    for (int u = 0; u < kFwdUnroll; ++u) halo_mass<NB, LOGSIG>(xs[u], ths[u], bins, acc, cnt);
+    for (int u = 0; u < kFwdUnroll; ++u) halo_mass<NB, LOGSIG, REL>(xs[u], ths[u], bins, acc, cnt);
   }
+#if MG_FWD_BALLOT
+  const bool counter = lane == 0;  // the counts are per wave: fold them in once
+#else
+  const bool counter = true;
+#endif
 #pragma unroll
-  for (int k = 0; k < NB; ++k) acc[k] += (float)(cnt[k + 1] - cnt[k]);
+  for (int k = 0; k < NB; ++k)
+    acc[k] = (acc[k + 1] - acc[k]) + (counter ? (float)(cnt[k + 1] - cnt[k]) : 0.0f);
   __shared__ float scratch[NB * (kThreads / kWave)];
-  block_sum_n<NB>(acc, scratch);
+  float(&bin)[NB] = *reinterpret_cast<float(*)[NB]>(acc);
+  block_sum_n<NB>(bin, scratch);
   if (threadIdx.x == 0) {
 #pragma unroll
     for (int k = 0; k < NB; ++k) slab[(int64_t)blockIdx.x * NB + k] = acc[k];
@@ -189,6 +211,16 @@ template <int NB, bool LOGSIG>
 __device__ __forceinline__ void halo_vjp(float x, float2 th, float inv, const float (&h)[NB + 1],
                                          const SmfBins& b, float& A, float& B) {
   const float nmi = -(x + th.x) * inv;
+#if MG_VJP_EXP == 2
+  // timing experiment: signed log-weight form (4 VALU/edge); numerically wrong here
+#pragma unroll
+  for (int e = 0; e <= NB; ++e) {
+    const float v = fmaf(b.edge[e], inv, (e & 1) ? -nmi : nmi);
+    const float g = fast_exp2(fmaf(-v, v, h[e]));
+    A = fmaf(b.scale[e & 15], g, A);
+    B = fmaf(g, v, B);
+  }
+#else
 #pragma unroll
   for (int e = 0; e <= NB; ++e) {
     const float w = fmaf(b.edge[e], inv, nmi);
@@ -196,6 +228,7 @@ __device__ __forceinline__ void halo_vjp(float x, float2 th, float inv, const fl
     A += t;
     B = fmaf(t, w, B);
   }
+#endif
 }
 
 // inv is the scaled inverse sigma (kWScale / sigma); A, B from halo_vjp.
@@ -279,6 +312,11 @@ __global__ __launch_bounds__(kThreads) void smf_vjp_tiles_kernel(
     }
   }
   __syncthreads();
+#if MG_VJP_EXP == 1
+  // timing experiment: phase 1 only
+  if (tid < t.p1 - t.p0) grad[t.p0 + tid] = s_ab[tid];
+  return;
+#endif
   // ---- phase 2: blocked per-thread sequential segmented reduction over <= kItems halos
   const int base = tid * kItems;
   const int cnt = (int)max((int64_t)0, min((int64_t)kItems, (t.h1 - t.h0) - base));
@@ -421,7 +459,14 @@ int smf_padded_bins(int64_t nb) { return padded_bins((int)nb); }
 
 // Grid that exactly fills the chip with resident forward workgroups (occupancy x CUs), so
 // the grid-stride loop runs in a single wave of workgroups without a partial tail round.
-int64_t smf_fwd_max_blocks(int64_t nb, bool log_sigma, bool has_pop) {
+// Runtime flags -> template arguments.
+template <typename F>
+static void with_bool(bool v, F&& f) {
+  if (v) f(std::true_type{});
+  else f(std::false_type{});
+}
+
+int64_t smf_fwd_max_blocks(int64_t nb, bool log_sigma, bool has_pop, bool rel_tail) {
   const int nbp = padded_bins((int)nb);
   int dev = 0;
   hipGetDevice(&dev);
@@ -429,9 +474,10 @@ int64_t smf_fwd_max_blocks(int64_t nb, bool log_sigma, bool has_pop) {
   hipGetDeviceProperties(&prop, dev);
   int occ = 0;
   MG_DISPATCH_NB(nbp, {
-    const void* f = log_sigma ? (has_pop ? (const void*)smf_fwd_kernel<NB, true, true> : (const void*)smf_fwd_kernel<NB, true, false>)
-                              : (has_pop ? (const void*)smf_fwd_kernel<NB, false, true> : (const void*)smf_fwd_kernel<NB, false, false>);
-    hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, f, kThreads, 0);
+    with_bool(log_sigma, [&](auto LS) { with_bool(has_pop, [&](auto HP) { with_bool(rel_tail, [&](auto RT) {
+      const void* f = (const void*)smf_fwd_kernel<NB, decltype(LS)::value, decltype(HP)::value, decltype(RT)::value>;
+      (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, f, kThreads, 0);
+    }); }); });
   });
   return (int64_t)std::max(1, occ) * prop.multiProcessorCount;
 }
@@ -439,7 +485,7 @@ int64_t smf_fwd_max_blocks(int64_t nb, bool log_sigma, bool has_pop) {
 // Forward over halos [begin, end); writes slab[nblocks * NBP].
 void smf_forward(torch::Tensor x, c10::optional<torch::Tensor> pop, torch::Tensor theta,
                  std::vector<double> edges, std::vector<double> scale, bool log_sigma,
-                 int64_t begin, int64_t end, torch::Tensor slab, int64_t nblocks) {
+                 int64_t begin, int64_t end, torch::Tensor slab, int64_t nblocks, bool rel_tail) {
   check_dev(x, "x", at::kFloat);
   check_dev(theta, "theta", at::kFloat);
   check_dev(slab, "slab", at::kFloat);
@@ -461,13 +507,10 @@ void smf_forward(torch::Tensor x, c10::optional<torch::Tensor> pop, torch::Tenso
   const float2* tp = reinterpret_cast<const float2*>(theta.data_ptr<float>());
   float* sp = slab.data_ptr<float>();
   MG_DISPATCH_NB(nbp, {
-    if (log_sigma) {
-      if (has_pop) hipLaunchKernelGGL((smf_fwd_kernel<NB, true, true>), dim3(nblocks), dim3(kThreads), 0, stream, xp, pp, tp, begin, end, b, sp);
-      else hipLaunchKernelGGL((smf_fwd_kernel<NB, true, false>), dim3(nblocks), dim3(kThreads), 0, stream, xp, pp, tp, begin, end, b, sp);
-    } else {
-      if (has_pop) hipLaunchKernelGGL((smf_fwd_kernel<NB, false, true>), dim3(nblocks), dim3(kThreads), 0, stream, xp, pp, tp, begin, end, b, sp);
-      else hipLaunchKernelGGL((smf_fwd_kernel<NB, false, false>), dim3(nblocks), dim3(kThreads), 0, stream, xp, pp, tp, begin, end, b, sp);
-    }
+    with_bool(log_sigma, [&](auto LS) { with_bool(has_pop, [&](auto HP) { with_bool(rel_tail, [&](auto RT) {
+      hipLaunchKernelGGL((smf_fwd_kernel<NB, decltype(LS)::value, decltype(HP)::value, decltype(RT)::value>),
+                         dim3(nblocks), dim3(kThreads), 0, stream, xp, pp, tp, begin, end, b, sp);
+    }); }); });
   });
 }
 

@@ -58,7 +58,7 @@ def _rank_range(n: int, rank: int, size: int):
 
 def make_population_data(num_params: int = 10_000_000, num_halos: int = 1 << 27, seed: int = 0,
                          comm=None, device=None, nbins: int = 10, chunks: int = 1,
-                         truth_offset=(0.1, 0.1)) -> dict:
+                         truth_offset=(0.1, 0.1), tail: str = "absolute") -> dict:
     """This rank's shard of the synthetic population-SMF data set.
 
     Returns a dict with the sorted device shard (``shard``), bins, volume, true
@@ -89,7 +89,7 @@ def make_population_data(num_params: int = 10_000_000, num_halos: int = 1 << 27,
     edges = np.linspace(8.5, 9.5, nbins + 1)
     # volume normalises the SMF to O(1e-2) per bin like the reference's tests
     volume = 10.0 * num_halos
-    return dict(shard=shard, bins=SmfBins.make(edges, volume), volume=volume, truth=truth,
+    return dict(shard=shard, bins=SmfBins.make(edges, volume, tail), volume=volume, truth=truth,
                 guess=guess, npop=npop, num_halos=int(num_halos), target_sumstats=None,
                 loss_eps=1e-10)
 
@@ -156,7 +156,7 @@ class PopulationSMFModel(OnePointModel):
         if self.shard.device.type != "cuda":
             return 1
         h0, h1 = self.shard.halo_range(chunk)
-        return self.shard.fwd_blocks(max(h1 - h0, 1), self.bins.nb, True)
+        return self.shard.fwd_blocks(max(h1 - h0, 1), self.bins.nb, True, self.bins.rel_tail)
 
     def engine_forward_chunk(self, theta, slab, chunk=None) -> int:
         return smf_forward_slab(theta, self.shard, self.bins, True, slab, chunk)

@@ -25,17 +25,33 @@ FWD_BLOCKS_MAX = 2048  # 8 workgroups per CU on 256 CUs, grid-stride beyond
 
 @dataclass(frozen=True)
 class SmfBins:
-    """Bin edges and per-bin scale ``1/(volume*width)`` of a stellar-mass function."""
+    """Bin edges and per-bin scale ``1/(volume*width)`` of a stellar-mass function.
+
+    ``tail`` selects the accuracy contract of the HIP forward's normal-CDF evaluation:
+    ``"absolute"`` (default): every edge CDF to 1.1e-7 absolute -- the accuracy of the
+    float32 ``erf`` the reference evaluates (tests/smf_example/smf_grad_descent.py:32-48);
+    ``"relative"``: every CDF tail to ~1.2e-6 *relative*, so bins fed only by the far
+    Gaussian tails of halos keep ~6 significant digits (the reference's float32 erf
+    difference loses them all); ~12% slower forward.
+    """
 
     edges: tuple
     scale: tuple
+    tail: str = "absolute"
 
     @staticmethod
-    def make(edges, volume: float) -> "SmfBins":
+    def make(edges, volume: float, tail: str = "absolute") -> "SmfBins":
+        if tail not in ("relative", "absolute"):
+            raise ValueError("tail must be 'relative' or 'absolute'")
         e = np.asarray(torch.as_tensor(edges).detach().cpu().double().numpy() if
                        isinstance(edges, torch.Tensor) else edges, dtype=np.float64)
         w = np.diff(e)
-        return SmfBins(tuple(float(v) for v in e), tuple(float(1.0 / (volume * d)) for d in w))
+        return SmfBins(tuple(float(v) for v in e), tuple(float(1.0 / (volume * d)) for d in w),
+                       tail)
+
+    @property
+    def rel_tail(self) -> bool:
+        return self.tail == "relative"
 
     @property
     def nb(self) -> int:
@@ -163,15 +179,17 @@ class PopulationShard:
             return 0, self.n
         return self.chunk_halos[chunk], self.chunk_halos[chunk + 1]
 
-    def fwd_blocks(self, nhalos: int, nbins: int = 10, log_sigma: bool = True) -> int:
+    def fwd_blocks(self, nhalos: int, nbins: int = 10, log_sigma: bool = True,
+                   rel_tail: bool = False) -> int:
         """Forward grid: enough 256-thread workgroups for the halos (4 per thread per
         iteration), capped at one fully resident wave of workgroups."""
         cap = FWD_BLOCKS_MAX
         if self.device.type == "cuda":
-            key = (nbins, bool(log_sigma), self.pop is not None)
+            key = (nbins, bool(log_sigma), self.pop is not None, bool(rel_tail))
             if key not in _GRID_CACHE:
                 _GRID_CACHE[key] = int(ext().smf_fwd_max_blocks(nbins, bool(log_sigma),
-                                                                self.pop is not None))
+                                                                self.pop is not None,
+                                                                bool(rel_tail)))
             cap = _GRID_CACHE[key]
         return int(max(1, min(cap, math.ceil(nhalos / 256))))
 
@@ -211,9 +229,9 @@ def smf_forward_slab(theta: torch.Tensor, shard: PopulationShard, bins: SmfBins,
         slab[:bins.nbp].zero_()
         slab[:bins.nb] = (row / sc).to(slab.dtype)  # unscaled bin sums (scale at reduce)
         return 1
-    nblk = shard.fwd_blocks(max(h1 - h0, 1), bins.nb, log_sigma)
+    nblk = shard.fwd_blocks(max(h1 - h0, 1), bins.nb, log_sigma, bins.rel_tail)
     ext().smf_forward(shard.x, shard.pop, theta, list(bins.edges), list(bins.scale),
-                      bool(log_sigma), h0, h1, slab, nblk)
+                      bool(log_sigma), h0, h1, slab, nblk, bins.rel_tail)
     return nblk
 
 
@@ -235,7 +253,7 @@ def smf_forward_into(theta: torch.Tensor, shard: PopulationShard, bins: SmfBins,
     """Partial sumstats of the shard (or one population chunk) into ``out[:nbp]``."""
     if slab is None:
         h0, h1 = shard.halo_range(chunk)
-        nblk = shard.fwd_blocks(max(h1 - h0, 1), bins.nb, log_sigma)
+        nblk = shard.fwd_blocks(max(h1 - h0, 1), bins.nb, log_sigma, bins.rel_tail)
         slab = torch.empty(nblk * bins.nbp, dtype=torch.float32, device=theta.device)
     nrows = smf_forward_slab(theta, shard, bins, log_sigma, slab, chunk)
     return smf_slab_reduce(slab, nrows, bins, out)

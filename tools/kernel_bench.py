@@ -19,6 +19,7 @@ def main():
     ap.add_argument("--params", type=int, default=10_000_000)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--tag", default="")
+    ap.add_argument("--tail", default="absolute", choices=["relative", "absolute"])
     a = ap.parse_args()
     import torch
     if a.so:
@@ -30,13 +31,13 @@ def main():
     from multigrad_amd.ops import smf as S
     from multigrad_amd.ops.adam import fused_adam_
     dev = torch.device("cuda", 0)
-    data = make_population_data(a.params, a.halos, seed=1, device=dev)
+    data = make_population_data(a.params, a.halos, seed=1, device=dev, tail=a.tail)
     model = PopulationSMFModel(aux_data=data)
     model.set_target_from_truth()
     shard, bins = data["shard"], data["bins"]
     th = data["guess"]
     out = torch.zeros(bins.nbp, device=dev)
-    nblk = shard.fwd_blocks(shard.n, bins.nb, True)
+    nblk = shard.fwd_blocks(shard.n, bins.nb, True, bins.rel_tail)
     slab = torch.zeros(nblk * bins.nbp, device=dev)
     h = torch.zeros(bins.nbp + 1, device=dev)
     loss = torch.zeros(1, device=dev)
