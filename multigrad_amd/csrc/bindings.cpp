@@ -22,6 +22,18 @@ void smf_vjp(torch::Tensor x, c10::optional<torch::Tensor> pop, torch::Tensor th
              torch::Tensor tiles, int64_t tile_begin, int64_t tile_end, torch::Tensor h,
              std::vector<double> edges, std::vector<double> scale, bool log_sigma,
              torch::Tensor grad, torch::Tensor partials, torch::Tensor giant);
+int64_t smf_fwd_lanes_max_blocks(int64_t nb, bool log_sigma, bool rel_tail, bool resid);
+void smf_lanes_pack(torch::Tensor xs, torch::Tensor slot_src, torch::Tensor slot_len,
+                    torch::Tensor group_base, torch::Tensor group_len, torch::Tensor xi);
+void smf_forward_lanes(torch::Tensor xi, torch::Tensor slot_pop, torch::Tensor group_base,
+                       torch::Tensor group_len, torch::Tensor theta, std::vector<double> edges,
+                       std::vector<double> scale, bool log_sigma, int64_t g0, int64_t g1,
+                       torch::Tensor slab, int64_t nblocks, bool rel_tail,
+                       c10::optional<torch::Tensor> resid);
+void smf_vjp_lanes(torch::Tensor slot_pop, torch::Tensor slot_part, torch::Tensor theta,
+                   torch::Tensor h, torch::Tensor resid, int64_t s0, int64_t s1,
+                   std::vector<double> scale, bool log_sigma, torch::Tensor grad,
+                   torch::Tensor partials, torch::Tensor giant);
 // adam.hip
 void fused_adam(torch::Tensor u, torch::Tensor m, torch::Tensor v, torch::Tensor g,
                 c10::optional<torch::Tensor> p, c10::optional<torch::Tensor> lo,
@@ -39,6 +51,8 @@ std::tuple<torch::Tensor, torch::Tensor, torch::Tensor, torch::Tensor, int64_t>
 build_tiles(torch::Tensor counts, std::vector<int64_t> breaks, int64_t tile_halos,
             int64_t tile_pops);
 std::tuple<torch::Tensor, torch::Tensor> sort_by_population(torch::Tensor pop, int64_t npop);
+std::vector<torch::Tensor> build_lanes(torch::Tensor counts, std::vector<int64_t> breaks,
+                                       int64_t window, int64_t lmax);
 }  // namespace mg
 
 PYBIND11_MODULE(_C, m) {
@@ -50,10 +64,15 @@ PYBIND11_MODULE(_C, m) {
   m.def("smf_edge_weights", &mg::smf_edge_weights);
   m.def("smf_logmse", &mg::smf_logmse);
   m.def("smf_vjp", &mg::smf_vjp);
+  m.def("smf_fwd_lanes_max_blocks", &mg::smf_fwd_lanes_max_blocks);
+  m.def("smf_lanes_pack", &mg::smf_lanes_pack);
+  m.def("smf_forward_lanes", &mg::smf_forward_lanes);
+  m.def("smf_vjp_lanes", &mg::smf_vjp_lanes);
   m.def("fused_adam", &mg::fused_adam);
   m.def("multi_dot", &mg::multi_dot);
   m.def("multi_dot_workspace", &mg::multi_dot_workspace);
   m.def("lincomb", &mg::lincomb);
   m.def("build_tiles", &mg::build_tiles);
   m.def("sort_by_population", &mg::sort_by_population);
+  m.def("build_lanes", &mg::build_lanes);
 }

@@ -114,4 +114,151 @@ std::tuple<torch::Tensor, torch::Tensor> sort_by_population(torch::Tensor pop, i
   return {order, counts};
 }
 
+
+// ---------------------------------------------------------------------------------
+// Lane schedule ("lanes" layout): one 64-wide wavefront processes a *group* of 64
+// population slots, one slot per lane, each lane walking its own slot's halos serially.
+// The halos of a group are stored interleaved (halo j of lane l at base + 64 j + l), so
+// every load is fully coalesced, a lane loads its (a, sigma) once per slot instead of
+// once per halo, and -- because a lane owns a whole population -- per-population sums
+// need no cross-lane segmentation at all.  To keep the lanes of a wave busy for the
+// same number of iterations, slots are sorted by halo count (descending) inside windows
+// of `window` consecutive populations (windows keep the gradient scatter local), then cut
+// into groups of 64; a group runs max(len) iterations and shorter lanes are padded with
+// a sentinel.  Populations with more than `lmax` halos are split into parts of <= lmax
+// halos ("virtual" slots); their per-part gradient partials are summed in a fixed order
+// by the finalize kernel.
+//
+// counts: int64 [J] halos per population (halos sorted by population, CPU).
+// breaks: population indices where a chunk ends (windows never straddle a chunk).
+// Returns (slot_pop int32 [S] (-1: empty), slot_src int64 [S] (first halo in the sorted
+//          array), slot_len int32 [S], slot_part int32 [S] (partial index or -1),
+//          group_base int64 [G+1] (offset of the group in the interleaved array; the last
+//          entry is its total length), group_len int32 [G], chunk_groups int64 [C+1],
+//          giant int32 [P,3] = {pop, part_begin, part_end}, chunk_giant int64 [C+1]).
+std::vector<torch::Tensor> build_lanes(torch::Tensor counts, std::vector<int64_t> breaks,
+                                       int64_t window, int64_t lmax) {
+  TORCH_CHECK(counts.device().is_cpu() && counts.scalar_type() == at::kLong, "counts: int64 CPU");
+  TORCH_CHECK(window >= 1 && lmax >= 1, "bad lane-schedule limits");
+  constexpr int64_t kLanes = 64;
+  auto c = counts.contiguous();
+  const int64_t* cnt = c.data_ptr<int64_t>();
+  const int64_t J = c.numel();
+  std::vector<int64_t> brk;
+  for (auto b : breaks)
+    if (b > 0 && b < J) brk.push_back(b);
+  std::sort(brk.begin(), brk.end());
+  brk.erase(std::unique(brk.begin(), brk.end()), brk.end());
+  brk.push_back(J);
+
+  std::vector<int64_t> off(J + 1, 0);
+  for (int64_t p = 0; p < J; ++p) {
+    TORCH_CHECK(cnt[p] >= 0, "negative population count");
+    off[p + 1] = off[p] + cnt[p];
+  }
+  struct Item {
+    int64_t len, pop, part, src;
+  };
+  std::vector<int32_t> slot_pop, slot_len, slot_part, giant;
+  std::vector<int64_t> slot_src, group_base{0}, chunk_groups{0}, chunk_giant{0};
+  std::vector<int32_t> group_len;
+  std::vector<Item> items;
+  int64_t nparts = 0;
+  int64_t p = 0;
+  // groups of the current chunk before emission: 64 slots each
+  struct Slot {
+    int32_t pop, len, part;
+    int64_t src;
+  };
+  std::vector<Slot> cslots;
+  std::vector<int64_t> cglen;
+  for (size_t bi = 0; bi < brk.size(); ++bi) {
+    const int64_t pend = brk[bi];
+    cslots.clear();
+    cglen.clear();
+    for (int64_t w0 = p; w0 < pend; w0 += window) {
+      const int64_t w1 = std::min(pend, w0 + window);
+      items.clear();
+      for (int64_t q = w0; q < w1; ++q) {
+        const int64_t n = cnt[q];
+        if (n > lmax) {
+          const int64_t k = (n + lmax - 1) / lmax;
+          for (int64_t i = 0; i < k; ++i)
+            items.push_back({std::min(lmax, n - i * lmax), q, i, off[q] + i * lmax});
+          // partial indices are contiguous per split population, in population order
+          giant.insert(giant.end(), {(int32_t)q, (int32_t)nparts, (int32_t)(nparts + k)});
+          nparts += k;
+        } else {
+          items.push_back({n, q, -1, off[q]});
+        }
+      }
+      std::stable_sort(items.begin(), items.end(), [](const Item& a, const Item& b) {
+        return a.len > b.len;
+      });
+      const size_t n_items = items.size();
+      const size_t padded = (n_items + kLanes - 1) / kLanes * kLanes;
+      for (size_t i = 0; i < padded; i += kLanes) {
+        int64_t glen = 0;
+        for (size_t l = 0; l < (size_t)kLanes; ++l) {
+          if (i + l < n_items) {
+            const Item& it = items[i + l];
+            // part i -> -1-i; whole population -> 0 (mapped to global indices below)
+            cslots.push_back({(int32_t)it.pop, (int32_t)it.len, -1 - (int32_t)it.part, it.src});
+            glen = std::max(glen, it.len);
+          } else {
+            cslots.push_back({-1, 0, 0, 0});
+          }
+        }
+        cglen.push_back(glen);
+      }
+    }
+    // Emit the chunk's groups longest first: a grid-stride over groups then hands every
+    // wavefront groups of nearly equal length in each round (static LPT balance).
+    std::vector<int64_t> order(cglen.size());
+    for (size_t g = 0; g < order.size(); ++g) order[g] = (int64_t)g;
+    std::stable_sort(order.begin(), order.end(),
+                     [&](int64_t a, int64_t b) { return cglen[a] > cglen[b]; });
+    for (int64_t g : order) {
+      for (int64_t l = 0; l < kLanes; ++l) {
+        const Slot& sl = cslots[g * kLanes + l];
+        slot_pop.push_back(sl.pop);
+        slot_len.push_back(sl.len);
+        slot_src.push_back(sl.src);
+        slot_part.push_back(sl.pop < 0 ? -1 : sl.part);
+      }
+      group_len.push_back((int32_t)cglen[g]);
+      group_base.push_back(group_base.back() + cglen[g] * kLanes);
+    }
+    p = pend;
+    chunk_groups.push_back((int64_t)group_len.size());
+    chunk_giant.push_back((int64_t)giant.size() / 3);
+  }
+  // part fix-up: slot_part held -1 - part_index_within_pop (or -1 - (-1) = 0 for whole
+  // populations); map to the global partial index giant[pop].part_begin + i.
+  {
+    std::vector<int32_t> part_begin(J, -1);
+    for (size_t g = 0; g < giant.size(); g += 3) part_begin[giant[g]] = giant[g + 1];
+    for (size_t s = 0; s < slot_pop.size(); ++s) {
+      const int32_t q = slot_pop[s];
+      if (q < 0 || part_begin[q] < 0) {
+        slot_part[s] = -1;
+      } else {
+        slot_part[s] = part_begin[q] + (-1 - slot_part[s]);
+      }
+    }
+  }
+  auto i32 = [](const std::vector<int32_t>& v) {
+    auto t = torch::empty({(int64_t)v.size()}, torch::kInt);
+    if (!v.empty()) std::memcpy(t.data_ptr<int32_t>(), v.data(), v.size() * sizeof(int32_t));
+    return t;
+  };
+  auto i64 = [](const std::vector<int64_t>& v) {
+    auto t = torch::empty({(int64_t)v.size()}, torch::kLong);
+    if (!v.empty()) std::memcpy(t.data_ptr<int64_t>(), v.data(), v.size() * sizeof(int64_t));
+    return t;
+  };
+  return {i32(slot_pop), i64(slot_src), i32(slot_len), i32(slot_part), i64(group_base),
+          i32(group_len), i64(chunk_groups), i32(giant).reshape({-1, 3}), i64(chunk_giant)};
+}
+
 }  // namespace mg

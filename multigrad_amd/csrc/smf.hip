@@ -414,6 +414,174 @@ __global__ __launch_bounds__(kThreads) void smf_vjp_finalize_kernel(
   if (threadIdx.x == 0) grad[c] = pop_grad<LOGSIG>(theta[c], (float)v[0], (float)v[1]);
 }
 
+// ================================================================== lanes layout
+// One wavefront per group of 64 population slots, one slot per lane (schedule built by
+// runtime.cpp:build_lanes).  Halo j of lane l lives at xi[group_base + 64 j + l]
+// (coalesced); lanes shorter than the group are padded with kLaneSentinel, which
+// contributes exactly zero everywhere (n -> -huge: Gaussian factor 0, sign bit set on
+// every edge so the integer parts cancel, and 0 * finite = 0 in the residuals).
+//
+// RESID: the forward also keeps, per slot and edge, the Gaussian-factor sums the VJP
+// needs -- G_e = sum_i exp2(-w_ie^2) and W_e = sum_i exp2(-w_ie^2) w_ie (w = -n) -- and
+// stores them group-major as residuals [ngroups][2 (NB+1)][64] (coalesced, one contiguous
+// block per group).  The VJP is then linear in the
+// edge weights: A = sum_e h_e G_e, B = sum_e h_e W_e, a memory-bound pass over 22
+// floats per population instead of a recomputation over every halo (what jax.vjp does
+// with its saved residuals, reference multigrad/multigrad.py:518-532).
+constexpr float kLaneSentinel = -1e30f;
+
+template <int NB, bool LOGSIG, bool REL, bool RESID>
+__device__ __forceinline__ void lane_halo(float x, float ninv, float mua, const SmfBins& b,
+                                          float (&acc)[NB + 1], int (&cnt)[NB + 1],
+                                          float (&G)[NB + 1], float (&W)[NB + 1]) {
+  const float mu = fmaf(x, -ninv, mua);  // (x + a) * kWScale / sigma
+#pragma unroll
+  for (int e = 0; e <= NB; ++e) {
+    const float n = fmaf(b.edge[e], ninv, mu);
+    float p, g;
+    normal_tail_parts_w<REL>(n, p, g);
+    acc[e] = fmaf(p, __builtin_copysignf(g, n), acc[e]);
+    cnt[e] += __builtin_popcountll(__builtin_amdgcn_ballot_w64(n < 0.0f));
+    if constexpr (RESID) {
+      G[e] += g;
+      W[e] = fmaf(-g, n, W[e]);
+    }
+  }
+}
+
+#ifndef MG_LANES_MINWAVES
+#define MG_LANES_MINWAVES 6
+#endif
+#ifndef MG_LANES_UNROLL
+#define MG_LANES_UNROLL 2
+#endif
+constexpr int kLanesUnroll = MG_LANES_UNROLL;
+
+template <int NB, bool LOGSIG, bool REL, bool RESID>
+__global__ __launch_bounds__(kThreads, MG_LANES_MINWAVES) void smf_fwd_lanes_kernel(
+    const float* __restrict__ xi, const int32_t* __restrict__ slot_pop,
+    const int64_t* __restrict__ group_base, const int32_t* __restrict__ group_len,
+    const float2* __restrict__ theta, int64_t g0, int64_t g1, SmfBins bins,
+    float* __restrict__ slab, float* __restrict__ resid) {
+  float acc[NB + 1];
+  int cnt[NB + 1];
+#pragma unroll
+  for (int k = 0; k <= NB; ++k) {
+    acc[k] = 0.0f;
+    cnt[k] = 0;
+  }
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t nwaves = (int64_t)gridDim.x * (kThreads / kWave);
+  // Software pipeline across groups as well as within one: the next group's parameters
+  // and first halos are loaded *before* this group's residual stores (so the in-order
+  // memory counter never makes the next group wait for those stores), and the slot ->
+  // population index is fetched one group further ahead, so the dependent theta gather
+  // does not wait for a load issued in the same transition.
+  int64_t g = g0 + (int64_t)blockIdx.x * (kThreads / kWave) + wid;
+  float2 th = make_float2(0.f, 0.f);
+  const float* xp = xi;
+  int len = 0;
+  int c_next = 0;
+  float xn[kLanesUnroll];
+  auto load_group = [&](int64_t gg, int c) {
+    th = theta[c < 0 ? 0 : c];
+    xp = xi + group_base[gg] + lane;
+    len = group_len[gg];
+#pragma unroll
+    for (int u = 0; u < kLanesUnroll; ++u) xn[u] = u < len ? xp[(int64_t)u * kWave] : kLaneSentinel;
+    const int64_t ga = gg + nwaves;
+    if (ga < g1) c_next = slot_pop[ga * kWave + lane];
+  };
+  if (g < g1) load_group(g, slot_pop[g * kWave + lane]);
+  while (g < g1) {
+    const float ninv = -inv_sigma<LOGSIG>(th.y) * kWScale;
+    const float mua = -th.x * ninv;
+    float G[NB + 1], W[NB + 1];
+#pragma unroll
+    for (int e = 0; e <= NB; ++e) {
+      G[e] = 0.0f;
+      W[e] = 0.0f;
+    }
+    // the next kLanesUnroll loads are in flight while the current halos are computed;
+    // past-the-end halos are the sentinel (exact zero contribution)
+    for (int j = 0; j < len; j += kLanesUnroll) {
+      float xc[kLanesUnroll];
+#pragma unroll
+      for (int u = 0; u < kLanesUnroll; ++u) {
+        xc[u] = xn[u];
+        const int jn = j + kLanesUnroll + u;
+        xn[u] = jn < len ? xp[(int64_t)jn * kWave] : kLaneSentinel;
+      }
+#pragma unroll
+      for (int u = 0; u < kLanesUnroll; ++u)
+        lane_halo<NB, LOGSIG, REL, RESID>(xc[u], ninv, mua, bins, acc, cnt, G, W);
+    }
+    const int64_t gn = g + nwaves;
+    if (gn < g1) load_group(gn, c_next);
+    if constexpr (RESID) {  // group-major [g][2 (NB+1)][64]: one contiguous block per group
+      float* rg = resid + g * (2 * (NB + 1) * kWave) + lane;
+#pragma unroll
+      for (int e = 0; e <= NB; ++e) {
+        rg[e * kWave] = G[e];
+        rg[(NB + 1 + e) * kWave] = W[e];
+      }
+    }
+    g = gn;
+  }
+  const bool counter = lane == 0;  // the counts are per wave: fold them in once
+#pragma unroll
+  for (int k = 0; k < NB; ++k)
+    acc[k] = (acc[k + 1] - acc[k]) + (counter ? (float)(cnt[k + 1] - cnt[k]) : 0.0f);
+  __shared__ float scratch[NB * (kThreads / kWave)];
+  float(&bin)[NB] = *reinterpret_cast<float(*)[NB]>(acc);
+  block_sum_n<NB>(bin, scratch);
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int k = 0; k < NB; ++k) slab[(int64_t)blockIdx.x * NB + k] = acc[k];
+  }
+}
+
+// Residual VJP over slots [s0, s1): whole populations write their gradient, parts of
+// split populations write partials[part] (summed by smf_vjp_finalize_kernel).
+template <int NB, bool LOGSIG>
+__global__ __launch_bounds__(kThreads) void smf_vjp_lanes_kernel(
+    const int32_t* __restrict__ slot_pop, const int32_t* __restrict__ slot_part,
+    const float2* __restrict__ theta, const float* __restrict__ hvec,
+    const float* __restrict__ resid, int64_t s0, int64_t s1,
+    float2* __restrict__ grad, float2* __restrict__ partials) {
+  const int64_t s = s0 + (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (s >= s1) return;
+  const int c = slot_pop[s];
+  const float* rg = resid + (s >> 6) * (2 * (NB + 1) * kWave) + (s & (kWave - 1));
+  float A = 0.0f, B = 0.0f;
+#pragma unroll
+  for (int e = 0; e <= NB; ++e) {
+    A = fmaf(hvec[e], rg[e * kWave], A);
+    B = fmaf(hvec[e], rg[(NB + 1 + e) * kWave], B);
+  }
+  if (c < 0) return;
+  const int part = slot_part[s];
+  if (part >= 0) partials[part] = make_float2(A, B);
+  else grad[c] = pop_grad<LOGSIG>(theta[c], A, B);
+}
+
+// Interleave the population-sorted halos into the lanes layout (one wave per group).
+__global__ __launch_bounds__(kThreads) void smf_lanes_pack_kernel(
+    const float* __restrict__ xs, const int64_t* __restrict__ slot_src,
+    const int32_t* __restrict__ slot_len, const int64_t* __restrict__ group_base,
+    const int32_t* __restrict__ group_len, int64_t ngroups, float* __restrict__ xi) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int64_t g = (int64_t)blockIdx.x * (kThreads / kWave) + (threadIdx.x >> 6);
+  if (g >= ngroups) return;
+  const int64_t s = g * kWave + lane;
+  const int64_t src = slot_src[s];
+  const int len = slot_len[s];
+  const int glen = group_len[g];
+  float* dst = xi + group_base[g] + lane;
+  for (int j = 0; j < glen; ++j) dst[(int64_t)j * kWave] = j < len ? xs[src + j] : kLaneSentinel;
+}
+
 // ------------------------------------------------------------------ host side
 static int padded_bins(int nb) {
   const int sizes[] = {1, 2, 4, 8, 10, 16, 32};
@@ -597,6 +765,128 @@ void smf_vjp(torch::Tensor x, c10::optional<torch::Tensor> pop, torch::Tensor th
         hipLaunchKernelGGL((smf_vjp_tiles_kernel<NB, true>), dim3(ntiles), dim3(kThreads), 0, stream, xp, pp, tp, tl, h.data_ptr<float>(), b, gp, pa);
       else
         hipLaunchKernelGGL((smf_vjp_tiles_kernel<NB, false>), dim3(ntiles), dim3(kThreads), 0, stream, xp, pp, tp, tl, h.data_ptr<float>(), b, gp, pa);
+    });
+  }
+  const int64_t ng = giant.numel() / 3;
+  if (ng > 0) {
+    check_dev(giant, "giant", at::kInt);
+    TORCH_CHECK(pa != nullptr, "partials buffer required");
+    if (log_sigma)
+      hipLaunchKernelGGL((smf_vjp_finalize_kernel<true>), dim3(ng), dim3(kThreads), 0, stream, giant.data_ptr<int32_t>(), pa, tp, gp);
+    else
+      hipLaunchKernelGGL((smf_vjp_finalize_kernel<false>), dim3(ng), dim3(kThreads), 0, stream, giant.data_ptr<int32_t>(), pa, tp, gp);
+  }
+}
+
+// ------------------------------------------------------------------ lanes host side
+int64_t smf_fwd_lanes_max_blocks(int64_t nb, bool log_sigma, bool rel_tail, bool resid) {
+  const int nbp = padded_bins((int)nb);
+  int dev = 0;
+  hipGetDevice(&dev);
+  hipDeviceProp_t prop;
+  hipGetDeviceProperties(&prop, dev);
+  int occ = 0;
+  MG_DISPATCH_NB(nbp, {
+    with_bool(log_sigma, [&](auto LS) { with_bool(rel_tail, [&](auto RT) { with_bool(resid, [&](auto RS) {
+      const void* f = (const void*)smf_fwd_lanes_kernel<NB, decltype(LS)::value, decltype(RT)::value, decltype(RS)::value>;
+      (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, f, kThreads, 0);
+    }); }); });
+  });
+  return (int64_t)std::max(1, occ) * prop.multiProcessorCount;
+}
+
+void smf_lanes_pack(torch::Tensor xs, torch::Tensor slot_src, torch::Tensor slot_len,
+                    torch::Tensor group_base, torch::Tensor group_len, torch::Tensor xi) {
+  check_dev(xs, "xs", at::kFloat);
+  check_dev(slot_src, "slot_src", at::kLong);
+  check_dev(slot_len, "slot_len", at::kInt);
+  check_dev(group_base, "group_base", at::kLong);
+  check_dev(group_len, "group_len", at::kInt);
+  check_dev(xi, "xi", at::kFloat);
+  const int64_t ng = group_len.numel();
+  TORCH_CHECK(group_base.numel() == ng + 1 && slot_src.numel() == ng * kWave &&
+                  slot_len.numel() == ng * kWave, "inconsistent lane schedule");
+  if (ng == 0) return;
+  const int64_t gpb = kThreads / kWave;
+  hipLaunchKernelGGL(smf_lanes_pack_kernel, dim3((ng + gpb - 1) / gpb), dim3(kThreads), 0,
+                     at::hip::getCurrentHIPStream(), xs.data_ptr<float>(),
+                     slot_src.data_ptr<int64_t>(), slot_len.data_ptr<int32_t>(),
+                     group_base.data_ptr<int64_t>(), group_len.data_ptr<int32_t>(), ng,
+                     xi.data_ptr<float>());
+}
+
+// Forward over groups [g0, g1) of the lanes layout; optional residuals [ngroups, 2(NBP+1), 64].
+void smf_forward_lanes(torch::Tensor xi, torch::Tensor slot_pop, torch::Tensor group_base,
+                       torch::Tensor group_len, torch::Tensor theta, std::vector<double> edges,
+                       std::vector<double> scale, bool log_sigma, int64_t g0, int64_t g1,
+                       torch::Tensor slab, int64_t nblocks, bool rel_tail,
+                       c10::optional<torch::Tensor> resid) {
+  check_dev(xi, "xi", at::kFloat);
+  check_dev(slot_pop, "slot_pop", at::kInt);
+  check_dev(group_base, "group_base", at::kLong);
+  check_dev(group_len, "group_len", at::kInt);
+  check_dev(theta, "theta", at::kFloat);
+  check_dev(slab, "slab", at::kFloat);
+  const int nbp = padded_bins((int)scale.size());
+  const int64_t ng = group_len.numel();
+  TORCH_CHECK(g0 >= 0 && g1 <= ng && g0 <= g1, "bad group range");
+  TORCH_CHECK(slot_pop.numel() == ng * kWave && group_base.numel() == ng + 1, "inconsistent lane schedule");
+  TORCH_CHECK(slab.numel() >= nblocks * nbp, "slab too small");
+  TORCH_CHECK(nblocks >= 1 && nblocks <= 65535, "bad block count");
+  const bool has_resid = resid.has_value() && resid->defined();
+  float* rp = nullptr;
+  if (has_resid) {
+    check_dev(*resid, "resid", at::kFloat);
+    TORCH_CHECK(resid->dim() == 3 && resid->size(0) == ng && resid->size(1) == 2 * (nbp + 1) &&
+                    resid->size(2) == kWave, "resid must be [ngroups, 2*(nbp+1), 64]");
+    rp = resid->data_ptr<float>();
+  }
+  const SmfBins b = make_bins(edges, scale, nbp);
+  auto stream = at::hip::getCurrentHIPStream();
+  const float2* tp = reinterpret_cast<const float2*>(theta.data_ptr<float>());
+  MG_DISPATCH_NB(nbp, {
+    with_bool(log_sigma, [&](auto LS) { with_bool(rel_tail, [&](auto RT) { with_bool(has_resid, [&](auto RS) {
+      hipLaunchKernelGGL((smf_fwd_lanes_kernel<NB, decltype(LS)::value, decltype(RT)::value, decltype(RS)::value>),
+                         dim3(nblocks), dim3(kThreads), 0, stream, xi.data_ptr<float>(),
+                         slot_pop.data_ptr<int32_t>(), group_base.data_ptr<int64_t>(),
+                         group_len.data_ptr<int32_t>(), tp, g0, g1, b, slab.data_ptr<float>(), rp);
+    }); }); });
+  });
+}
+
+// Residual VJP over slots [s0, s1) plus the fixed-order finalize of split populations
+// listed in giant [G,3] = {pop, part_begin, part_end}.
+void smf_vjp_lanes(torch::Tensor slot_pop, torch::Tensor slot_part, torch::Tensor theta,
+                   torch::Tensor h, torch::Tensor resid, int64_t s0, int64_t s1,
+                   std::vector<double> scale, bool log_sigma, torch::Tensor grad,
+                   torch::Tensor partials, torch::Tensor giant) {
+  check_dev(slot_pop, "slot_pop", at::kInt);
+  check_dev(slot_part, "slot_part", at::kInt);
+  check_dev(theta, "theta", at::kFloat);
+  check_dev(h, "h", at::kFloat);
+  check_dev(resid, "resid", at::kFloat);
+  check_dev(grad, "grad", at::kFloat);
+  const int nbp = padded_bins((int)scale.size());
+  TORCH_CHECK(h.numel() >= nbp + 1, "h too small");
+  TORCH_CHECK(grad.numel() == theta.numel(), "grad/theta size mismatch");
+  const int64_t ns = slot_pop.numel();
+  TORCH_CHECK(slot_part.numel() == ns && resid.dim() == 3 && resid.size(0) * kWave == ns &&
+                  resid.size(1) == 2 * (nbp + 1) && resid.size(2) == kWave, "inconsistent residuals");
+  TORCH_CHECK(s0 >= 0 && s1 <= ns && s0 <= s1, "bad slot range");
+  auto stream = at::hip::getCurrentHIPStream();
+  const float2* tp = reinterpret_cast<const float2*>(theta.data_ptr<float>());
+  float2* gp = reinterpret_cast<float2*>(grad.data_ptr<float>());
+  float2* pa = partials.numel() ? reinterpret_cast<float2*>(partials.data_ptr<float>()) : nullptr;
+  TORCH_CHECK(s0 % kWave == 0 && s1 % kWave == 0, "slot ranges must be group aligned");
+  TORCH_CHECK(resid.is_contiguous(), "resid must be contiguous");
+  if (s1 > s0) {
+    const int64_t nblk = (s1 - s0 + kThreads - 1) / kThreads;
+    MG_DISPATCH_NB(nbp, {
+      with_bool(log_sigma, [&](auto LS) {
+        hipLaunchKernelGGL((smf_vjp_lanes_kernel<NB, decltype(LS)::value>), dim3(nblk), dim3(kThreads), 0,
+                           stream, slot_pop.data_ptr<int32_t>(), slot_part.data_ptr<int32_t>(), tp,
+                           h.data_ptr<float>(), resid.data_ptr<float>(), s0, s1, gp, pa);
+      });
     });
   }
   const int64_t ng = giant.numel() / 3;

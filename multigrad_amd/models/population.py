@@ -58,7 +58,8 @@ def _rank_range(n: int, rank: int, size: int):
 
 def make_population_data(num_params: int = 10_000_000, num_halos: int = 1 << 27, seed: int = 0,
                          comm=None, device=None, nbins: int = 10, chunks: int = 1,
-                         truth_offset=(0.1, 0.1), tail: str = "absolute") -> dict:
+                         truth_offset=(0.1, 0.1), tail: str = "absolute",
+                         layout: str = "lanes") -> dict:
     """This rank's shard of the synthetic population-SMF data set.
 
     Returns a dict with the sorted device shard (``shard``), bins, volume, true
@@ -77,7 +78,8 @@ def make_population_data(num_params: int = 10_000_000, num_halos: int = 1 << 27,
     q = 0.9 * hash_uniform(idx, seed + 1)
     logm = (10.0 - torch.log10(1.0 - q)).to(torch.float32)          # log10(1e10/(1-q))
     del idx, q
-    shard = PopulationShard(logm, pop.to(torch.int32), npop, device=device, chunks=chunks)
+    shard = PopulationShard(logm, pop.to(torch.int32), npop, device=device, chunks=chunks,
+                            layout=layout)
     del logm, pop
     cidx = torch.arange(npop, dtype=torch.int64, device=device)
     truth = torch.empty(2 * npop, dtype=torch.float32, device=device)
@@ -156,10 +158,13 @@ class PopulationSMFModel(OnePointModel):
         if self.shard.device.type != "cuda":
             return 1
         h0, h1 = self.shard.halo_range(chunk)
-        return self.shard.fwd_blocks(max(h1 - h0, 1), self.bins.nb, True, self.bins.rel_tail)
+        return self.shard.fwd_blocks(max(h1 - h0, 1), self.bins.nb, True, self.bins.rel_tail,
+                                     chunk)
 
     def engine_forward_chunk(self, theta, slab, chunk=None) -> int:
-        return smf_forward_slab(theta, self.shard, self.bins, True, slab, chunk)
+        # the engine always runs the VJP of a chunk after this forward at the same theta,
+        # so the forward stores the VJP residuals (lanes layout)
+        return smf_forward_slab(theta, self.shard, self.bins, True, slab, chunk, resid=True)
 
     def engine_reduce(self, slab, nrows, S):
         return smf_slab_reduce(slab, nrows, self.bins, S)
@@ -182,7 +187,8 @@ class PopulationSMFModel(OnePointModel):
                          loss_out, self._empty, h_out)
 
     def engine_vjp_into(self, theta, h, grad, chunk=None):
-        return smf_vjp_into(theta, self.shard, self.bins, True, h, grad, chunk=chunk)
+        return smf_vjp_into(theta, self.shard, self.bins, True, h, grad, chunk=chunk,
+                            residuals_ready=True)
 
     # simple (unchunked) protocol helpers
     def engine_partial_into(self, theta, out, slab=None, chunk=None):

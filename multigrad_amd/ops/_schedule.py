@@ -52,3 +52,63 @@ def build_tiles_py(counts, breaks, tile_halos: int, tile_pops: int):
         t[i, 3] = slot & 0xFFFFFFFF
     g = torch.tensor(giant, dtype=torch.int32).reshape(-1, 3)
     return t, g, torch.tensor(chunk_tiles), torch.tensor(chunk_giant), nslots
+
+
+def build_lanes_py(counts, breaks, window: int, lmax: int):
+    """Mirror of ``csrc/runtime.cpp:build_lanes`` (lanes layout schedule); same outputs."""
+    lanes = 64
+    cnt = np.asarray(torch.as_tensor(counts).cpu().numpy(), dtype=np.int64)
+    J = cnt.size
+    brk = sorted({int(b) for b in breaks if 0 < int(b) < J}) + [J]
+    off = np.zeros(J + 1, dtype=np.int64)
+    off[1:] = np.cumsum(cnt)
+    slot_pop, slot_src, slot_len, slot_part = [], [], [], []
+    group_base, group_len = [0], []
+    chunk_groups, chunk_giant = [0], [0]
+    giant = []
+    part_begin = {}
+    nparts = 0
+    p = 0
+    for pend in brk:
+        cgroups = []  # (glen, [64 slot tuples]) of this chunk
+        for w0 in range(p, pend, window):
+            w1 = min(pend, w0 + window)
+            items = []
+            for q in range(w0, w1):
+                n = int(cnt[q])
+                if n > lmax:
+                    k = -(-n // lmax)
+                    items += [(min(lmax, n - i * lmax), q, i, int(off[q]) + i * lmax) for i in range(k)]
+                    giant.append((q, nparts, nparts + k))
+                    part_begin[q] = nparts
+                    nparts += k
+                else:
+                    items.append((n, q, -1, int(off[q])))
+            items.sort(key=lambda it: -it[0])  # stable: ties keep population/part order
+            padded = -(-len(items) // lanes) * lanes
+            for i in range(0, padded, lanes):
+                slots = []
+                for l in range(lanes):
+                    if i + l < len(items):
+                        n, q, part, src = items[i + l]
+                        slots.append((q, n, src, part_begin[q] + part if part >= 0 else -1))
+                    else:
+                        slots.append((-1, 0, 0, -1))
+                cgroups.append((max(sl[1] for sl in slots), slots))
+        cgroups.sort(key=lambda g: -g[0])  # longest groups first (stable)
+        for glen, slots in cgroups:
+            for q, n, src, part in slots:
+                slot_pop.append(q)
+                slot_len.append(n)
+                slot_src.append(src)
+                slot_part.append(part)
+            group_len.append(glen)
+            group_base.append(group_base[-1] + glen * lanes)
+        p = pend
+        chunk_groups.append(len(group_len))
+        chunk_giant.append(len(giant))
+    i32 = lambda v: torch.tensor(v, dtype=torch.int32)  # noqa: E731
+    i64 = lambda v: torch.tensor(v, dtype=torch.int64)  # noqa: E731
+    g = torch.tensor(giant, dtype=torch.int32).reshape(-1, 3)
+    return [i32(slot_pop), i64(slot_src), i32(slot_len), i32(slot_part), i64(group_base),
+            i32(group_len), i64(chunk_groups), g, i64(chunk_giant)]

@@ -21,6 +21,8 @@ __all__ = ["SmfBins", "PopulationShard", "smf_sumstats", "smf_sumstats_reference
 TILE_HALOS = 2048
 TILE_POPS = 2048
 FWD_BLOCKS_MAX = 2048  # 8 workgroups per CU on 256 CUs, grid-stride beyond
+LANE_WINDOW = 4096     # lanes layout: populations sorted by size within windows of this many
+LANE_LMAX = 4096       # lanes layout: populations with more halos are split into parts
 
 
 @dataclass(frozen=True)
@@ -111,13 +113,28 @@ class PopulationShard:
     device : device for the kernels
     chunks : number of contiguous population chunks (tiles never straddle a chunk, so
         per-chunk VJPs can overlap per-chunk gradient collectives)
+    layout : device layout of a population shard on the GPU.
+        ``"lanes"`` (default with populations): one wavefront lane per population slot,
+        halos interleaved per 64-slot group (runtime.cpp:build_lanes); the forward keeps
+        per-population residuals and the VJP is a memory-bound pass over them.
+        ``"tiles"``: halos sorted by population, segmented-scan VJP over a tile schedule
+        that recomputes every halo (no residual memory).  Shared-parameter shards
+        (``pop=None``) always use the plain halo array.
     """
 
     def __init__(self, x, pop=None, npop: int = 1, device=None, chunks: int = 1,
-                 tile_halos: int = TILE_HALOS, tile_pops: int = TILE_POPS):
+                 tile_halos: int = TILE_HALOS, tile_pops: int = TILE_POPS,
+                 layout: str = "lanes", lane_window: int = LANE_WINDOW,
+                 lane_lmax: int = LANE_LMAX):
         x = torch.as_tensor(x)
         device = torch.device(device) if device is not None else x.device
         self.device = device
+        if layout not in ("lanes", "tiles"):
+            raise ValueError("layout must be 'lanes' or 'tiles'")
+        self.layout = layout if (pop is not None and device.type == "cuda") else "tiles"
+        self._lane_window, self._lane_lmax = int(lane_window), int(lane_lmax)
+        self.resid = None          # lanes: [ngroups, 2 (nbp+1), 64] residuals of the last forward
+        self.resid_epoch = 0       # bumped by every residual-writing forward
         self.npop = int(npop)
         self.n = int(x.numel())
         if pop is None:
@@ -156,6 +173,9 @@ class PopulationShard:
         self.nchunks = len(pb) - 1
         self.chunk_pops = pb
         self.chunk_halos = [int(self.offsets[b]) for b in pb]
+        if self.layout == "lanes":
+            self._build_lanes(pb)
+            return
         if self.device.type != "cuda":
             self.tiles = torch.zeros((0, 4), dtype=torch.int64)
             self.giant = torch.zeros((0, 3), dtype=torch.int32)
@@ -174,15 +194,62 @@ class PopulationShard:
         self.partials = torch.zeros(max(self.nslots, 1) * 2, dtype=torch.float32,
                                     device=self.device)
 
+    def _build_lanes(self, pb) -> None:
+        from ._schedule import build_lanes_py
+        try:
+            out = ext().build_lanes(self.counts.to(torch.int64), list(pb[1:-1]),
+                                    self._lane_window, self._lane_lmax)
+        except ImportError:
+            out = build_lanes_py(self.counts, pb[1:-1], self._lane_window, self._lane_lmax)
+        (slot_pop, slot_src, slot_len, slot_part, group_base, group_len, chunk_groups, giant,
+         chunk_giant) = out
+        dev = self.device
+        self.nslots = int(slot_pop.numel())
+        self.ngroups = int(group_len.numel())
+        self.chunk_groups = [int(v) for v in chunk_groups]
+        self.chunk_giant = [int(v) for v in chunk_giant]
+        self.slot_pop = slot_pop.to(dev)
+        self.slot_part = slot_part.to(dev)
+        self.group_base = group_base.to(dev)
+        self.group_len = group_len.to(dev)
+        self.giant = giant.to(dev).contiguous()
+        nparts = int(giant[:, 2].max()) if giant.numel() else 0
+        self.partials = torch.zeros(max(nparts, 1) * 2, dtype=torch.float32, device=dev)
+        self.xi = torch.empty(int(group_base[-1]), dtype=torch.float32, device=dev)
+        ext().smf_lanes_pack(self.x, slot_src.to(dev), slot_len.to(dev), self.group_base,
+                             self.group_len, self.xi)
+        self.resid = None
+        self.resid_epoch += 1
+
+    def resid_buffer(self, nbp: int) -> torch.Tensor:
+        """Residual storage of the lanes forward, group-major [ngroups, 2 (nbp+1), 64]."""
+        shape = (self.ngroups, 2 * (nbp + 1), 64)
+        if self.resid is None or tuple(self.resid.shape) != shape:
+            self.resid = torch.empty(shape, dtype=torch.float32, device=self.device)
+        return self.resid
+
+    def group_range(self, chunk: Optional[int] = None):
+        if chunk is None:
+            return 0, self.ngroups
+        return self.chunk_groups[chunk], self.chunk_groups[chunk + 1]
+
     def halo_range(self, chunk: Optional[int] = None):
         if chunk is None:
             return 0, self.n
         return self.chunk_halos[chunk], self.chunk_halos[chunk + 1]
 
     def fwd_blocks(self, nhalos: int, nbins: int = 10, log_sigma: bool = True,
-                   rel_tail: bool = False) -> int:
-        """Forward grid: enough 256-thread workgroups for the halos (4 per thread per
-        iteration), capped at one fully resident wave of workgroups."""
+                   rel_tail: bool = False, chunk: Optional[int] = None) -> int:
+        """Forward grid: enough 256-thread workgroups for the halos (tiles layout) or for
+        the 64-slot groups (lanes layout, one per wavefront), capped at one fully
+        resident wave of workgroups."""
+        if self.layout == "lanes":
+            g0, g1 = self.group_range(chunk)
+            key = ("lanes", nbins, bool(log_sigma), bool(rel_tail))
+            if key not in _GRID_CACHE:
+                _GRID_CACHE[key] = int(ext().smf_fwd_lanes_max_blocks(
+                    nbins, bool(log_sigma), bool(rel_tail), True))
+            return int(max(1, min(_GRID_CACHE[key], math.ceil(max(g1 - g0, 1) / 4))))
         cap = FWD_BLOCKS_MAX
         if self.device.type == "cuda":
             key = (nbins, bool(log_sigma), self.pop is not None, bool(rel_tail))
@@ -216,9 +283,10 @@ def _build_tiles(counts, breaks, tile_halos, tile_pops):
 
 # ---------------------------------------------------------------------------- device ops
 def smf_forward_slab(theta: torch.Tensor, shard: PopulationShard, bins: SmfBins, log_sigma: bool,
-                     slab: torch.Tensor, chunk: Optional[int] = None) -> int:
+                     slab: torch.Tensor, chunk: Optional[int] = None, resid: bool = False) -> int:
     """Forward of the shard (or one population chunk) into per-workgroup slab rows;
-    returns the number of rows written.  CPU: one row from the PyTorch reference."""
+    returns the number of rows written.  CPU: one row from the PyTorch reference.
+    ``resid`` (lanes layout): also store the VJP residuals of these populations."""
     h0, h1 = shard.halo_range(chunk)
     if theta.device.type != "cuda":
         with torch.no_grad():
@@ -229,7 +297,16 @@ def smf_forward_slab(theta: torch.Tensor, shard: PopulationShard, bins: SmfBins,
         slab[:bins.nbp].zero_()
         slab[:bins.nb] = (row / sc).to(slab.dtype)  # unscaled bin sums (scale at reduce)
         return 1
-    nblk = shard.fwd_blocks(max(h1 - h0, 1), bins.nb, log_sigma, bins.rel_tail)
+    nblk = shard.fwd_blocks(max(h1 - h0, 1), bins.nb, log_sigma, bins.rel_tail, chunk)
+    if shard.layout == "lanes":
+        g0, g1 = shard.group_range(chunk)
+        rbuf = shard.resid_buffer(bins.nbp) if resid else None
+        ext().smf_forward_lanes(shard.xi, shard.slot_pop, shard.group_base, shard.group_len,
+                                theta, list(bins.edges), list(bins.scale), bool(log_sigma),
+                                g0, g1, slab, nblk, bins.rel_tail, rbuf)
+        if resid:
+            shard.resid_epoch += 1
+        return nblk
     ext().smf_forward(shard.x, shard.pop, theta, list(bins.edges), list(bins.scale),
                       bool(log_sigma), h0, h1, slab, nblk, bins.rel_tail)
     return nblk
@@ -249,20 +326,26 @@ def smf_slab_reduce(slab: torch.Tensor, nrows: int, bins: SmfBins, out: torch.Te
 
 def smf_forward_into(theta: torch.Tensor, shard: PopulationShard, bins: SmfBins, log_sigma: bool,
                      out: torch.Tensor, slab: Optional[torch.Tensor] = None,
-                     chunk: Optional[int] = None) -> torch.Tensor:
+                     chunk: Optional[int] = None, resid: bool = False) -> torch.Tensor:
     """Partial sumstats of the shard (or one population chunk) into ``out[:nbp]``."""
     if slab is None:
         h0, h1 = shard.halo_range(chunk)
-        nblk = shard.fwd_blocks(max(h1 - h0, 1), bins.nb, log_sigma, bins.rel_tail)
+        nblk = shard.fwd_blocks(max(h1 - h0, 1), bins.nb, log_sigma, bins.rel_tail, chunk)
         slab = torch.empty(nblk * bins.nbp, dtype=torch.float32, device=theta.device)
-    nrows = smf_forward_slab(theta, shard, bins, log_sigma, slab, chunk)
+    nrows = smf_forward_slab(theta, shard, bins, log_sigma, slab, chunk, resid)
     return smf_slab_reduce(slab, nrows, bins, out)
 
 
 def smf_vjp_into(theta: torch.Tensor, shard: PopulationShard, bins: SmfBins, log_sigma: bool,
-                 h: torch.Tensor, grad: torch.Tensor, chunk: Optional[int] = None) -> torch.Tensor:
+                 h: torch.Tensor, grad: torch.Tensor, chunk: Optional[int] = None,
+                 residuals_ready: bool = False) -> torch.Tensor:
     """Per-population VJP with edge weights ``h`` into ``grad`` (the chunk's parameters
-    only).  CPU: autograd of the PyTorch reference restricted to the chunk's halos."""
+    only).  CPU: autograd of the PyTorch reference restricted to the chunk's halos.
+
+    Lanes layout: the VJP reads the residuals of a forward at the same ``theta``.  Pass
+    ``residuals_ready=True`` only when the caller has just run
+    ``smf_forward_*(..., resid=True)`` at this ``theta`` for this chunk (the fused engine
+    does); otherwise the residual forward is recomputed here first."""
     if theta.device.type != "cuda":
         h0, h1 = shard.halo_range(chunk)
         p0, p1 = (0, shard.npop) if chunk is None else (shard.chunk_pops[chunk], shard.chunk_pops[chunk + 1])
@@ -284,6 +367,18 @@ def smf_vjp_into(theta: torch.Tensor, shard: PopulationShard, bins: SmfBins, log
         grad.reshape(-1)[2 * p0:2 * p1] = g[2 * p0:2 * p1].to(grad.dtype)
         return grad
     E = ext()
+    if shard.layout == "lanes":
+        if not residuals_ready or shard.resid is None:
+            nblk = shard.fwd_blocks(1, bins.nb, log_sigma, bins.rel_tail, chunk)
+            slab = torch.empty(nblk * bins.nbp, dtype=torch.float32, device=theta.device)
+            smf_forward_slab(theta, shard, bins, log_sigma, slab, chunk, resid=True)
+        g0, g1 = shard.group_range(chunk)
+        k0, k1 = (0, shard.giant.shape[0]) if chunk is None else \
+            (shard.chunk_giant[chunk], shard.chunk_giant[chunk + 1])
+        E.smf_vjp_lanes(shard.slot_pop, shard.slot_part, theta, h, shard.resid_buffer(bins.nbp),
+                        64 * g0, 64 * g1, list(bins.scale), bool(log_sigma), grad,
+                        shard.partials, shard.giant[k0:k1])
+        return grad
     if chunk is None:
         t0, t1 = 0, shard.tiles.shape[0]
         g0, g1 = 0, shard.giant.shape[0]
@@ -313,8 +408,10 @@ class _SmfSumstats(torch.autograd.Function):
     @staticmethod
     def forward(ctx, theta, shard, bins, log_sigma):
         out = torch.empty(bins.nbp, dtype=torch.float32, device=theta.device)
-        smf_forward_into(theta.detach().contiguous(), shard, bins, log_sigma, out)
+        resid = theta.requires_grad and shard.layout == "lanes"
+        smf_forward_into(theta.detach().contiguous(), shard, bins, log_sigma, out, resid=resid)
         ctx.shard, ctx.bins, ctx.log_sigma = shard, bins, log_sigma
+        ctx.epoch = shard.resid_epoch if resid else None
         ctx.save_for_backward(theta)
         return out[:bins.nb].clone()
 
@@ -326,7 +423,10 @@ class _SmfSumstats(torch.autograd.Function):
         h = torch.empty(bins.nbp + 1, dtype=torch.float32, device=theta.device)
         smf_edge_weights_into(g, bins, h)
         grad = torch.empty_like(theta, dtype=torch.float32)
-        smf_vjp_into(theta.detach().contiguous(), ctx.shard, bins, ctx.log_sigma, h, grad)
+        # residuals are still those of this forward unless another forward ran since
+        ready = ctx.epoch is not None and ctx.epoch == ctx.shard.resid_epoch
+        smf_vjp_into(theta.detach().contiguous(), ctx.shard, bins, ctx.log_sigma, h, grad,
+                     residuals_ready=ready)
         return grad.to(theta.dtype), None, None, None
 
 

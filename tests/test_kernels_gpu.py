@@ -28,14 +28,17 @@ def _theta(npop, seed=1, dtype=torch.float64):
     return th
 
 
+@pytest.mark.parametrize("layout", ["lanes", "tiles"])
 @pytest.mark.parametrize("nbins", [10, 7, 3])
 @pytest.mark.parametrize("giant", [None, 3])
-def test_population_forward_and_vjp_match_fp64(nbins, giant):
+def test_population_forward_and_vjp_match_fp64(nbins, giant, layout):
     n, npop = 200_000, 300
     x, pop = _rand_shard(n, npop, giant=giant)
     theta64 = _theta(npop)
     bins = S.SmfBins.make(np.linspace(8.0, 9.6, nbins + 1), volume=1e4)
-    shard = S.PopulationShard(x.float(), pop.int().to(DEV), npop, device=DEV, chunks=3)
+    shard = S.PopulationShard(x.float(), pop.int().to(DEV), npop, device=DEV, chunks=3,
+                              layout=layout)
+    assert shard.layout == layout
     # fp64 oracle on the same (float32-rounded) inputs
     xf = x.float().double()
     th_ref = theta64.float().double().requires_grad_(True)
@@ -74,10 +77,12 @@ def test_shared_params_model_kernel(log_sigma, tail):
     np.testing.assert_allclose(gk.cpu().double(), gref, rtol=5e-5)
 
 
-def test_forward_is_deterministic_and_chunks_sum():
+@pytest.mark.parametrize("layout", ["lanes", "tiles"])
+def test_forward_is_deterministic_and_chunks_sum(layout):
     n, npop = 100_000, 500
     x, pop = _rand_shard(n, npop, seed=5)
-    shard = S.PopulationShard(x.float(), pop.int().to(DEV), npop, device=DEV, chunks=4)
+    shard = S.PopulationShard(x.float(), pop.int().to(DEV), npop, device=DEV, chunks=4,
+                              layout=layout)
     th = _theta(npop).float().to(DEV)
     bins = S.SmfBins.make(np.linspace(8.0, 9.6, 11), volume=1e4)
     a = S.smf_sumstats(th, shard, bins)
@@ -221,3 +226,38 @@ def test_device_lbfgs_population_engine():
     from multigrad_amd.optim.lbfgs import run_lbfgs_device
     res2 = run_lbfgs_device(model.calc_loss_and_grad_from_params, data["guess"], maxsteps=40)
     assert res2.fun < 1e-3 * f0
+
+
+def test_lanes_matches_tiles_and_residual_reuse():
+    """The two layouts agree; the engine-style residual VJP equals the recomputing one;
+    a stale-residual backward (another forward in between) is detected and recomputed."""
+    n, npop = 150_000, 4000
+    x, pop = _rand_shard(n, npop, seed=9, giant=7)
+    th = _theta(npop).float().to(DEV)
+    bins = S.SmfBins.make(np.linspace(8.0, 9.6, 11), volume=1e4)
+    sl = S.PopulationShard(x.float(), pop.int().to(DEV), npop, device=DEV, layout="lanes",
+                           lane_window=256, lane_lmax=1000)
+    st = S.PopulationShard(x.float(), pop.int().to(DEV), npop, device=DEV, layout="tiles")
+    assert sl.giant.shape[0] == 1  # the giant population is split into parts
+    h = torch.randn(bins.nbp + 1, device=DEV)
+    out_l = torch.zeros(bins.nbp, device=DEV)
+    out_t = torch.zeros(bins.nbp, device=DEV)
+    S.smf_forward_into(th, sl, bins, True, out_l, resid=True)
+    S.smf_forward_into(th, st, bins, True, out_t)
+    torch.testing.assert_close(out_l, out_t, rtol=2e-6, atol=0)
+    g_ready = torch.zeros_like(th)
+    S.smf_vjp_into(th, sl, bins, True, h, g_ready, residuals_ready=True)
+    g_re = torch.zeros_like(th)
+    S.smf_vjp_into(th, sl, bins, True, h, g_re)
+    g_t = torch.zeros_like(th)
+    S.smf_vjp_into(th, st, bins, True, h, g_t)
+    assert torch.equal(g_ready, g_re)
+    torch.testing.assert_close(g_ready, g_t, rtol=1e-4, atol=1e-5 * float(g_t.abs().max()))
+    # stale residuals: forward at th, another residual forward at th2, backward at th
+    thr = th.clone().requires_grad_(True)
+    out = S.smf_sumstats(thr, sl, bins)
+    S.smf_sumstats((th + 0.05).requires_grad_(True), sl, bins)
+    (gk,) = torch.autograd.grad(out, thr, torch.ones_like(out))
+    thr2 = th.clone().requires_grad_(True)
+    (gk2,) = torch.autograd.grad(S.smf_sumstats(thr2, sl, bins), thr2, torch.ones_like(out))
+    assert torch.equal(gk, gk2)

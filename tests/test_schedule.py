@@ -1,0 +1,72 @@
+"""Host-side schedules for the SMF kernels (runtime.cpp vs its Python mirror, and the
+invariants the kernels rely on).  CPU only."""
+import numpy as np
+import pytest
+import torch
+
+from multigrad_amd.ops import _ext
+from multigrad_amd.ops._schedule import build_lanes_py, build_tiles_py
+
+
+def _counts(J, seed=0):
+    rng = np.random.default_rng(seed)
+    c = torch.tensor(rng.poisson(27, J), dtype=torch.int64)
+    if J > 20:
+        c[3] = 5000   # split into parts
+        c[11] = 0     # empty population
+        c[J - 1] = 130
+    return c
+
+
+@pytest.mark.parametrize("J,window,lmax,breaks", [(2000, 256, 100, [500, 501, 1500]),
+                                                   (3000, 4096, 4096, []), (1, 64, 10, []),
+                                                   (0, 64, 10, [])])
+def test_lanes_schedule_invariants(J, window, lmax, breaks):
+    counts = _counts(J)
+    (pop, src, ln, part, base, glen, cg, giant, cgi) = build_lanes_py(counts, breaks, window, lmax)
+    nchunks = len(sorted({b for b in breaks if 0 < b < J})) + 1
+    assert len(cg) == nchunks + 1 and len(cgi) == nchunks + 1
+    ng = glen.numel()
+    assert pop.numel() == 64 * ng and base.numel() == ng + 1
+    # every halo of every population is covered exactly once
+    off = np.concatenate([[0], np.cumsum(counts.numpy())])
+    cover = np.zeros(int(off[-1]), dtype=np.int64)
+    for s in range(pop.numel()):
+        q = int(pop[s])
+        if q < 0:
+            assert int(ln[s]) == 0
+            continue
+        a = int(src[s])
+        assert off[q] <= a and a + int(ln[s]) <= off[q + 1]
+        cover[a:a + int(ln[s])] += 1
+        assert int(ln[s]) <= lmax
+    assert (cover == 1).all()
+    # every population has a slot (so its gradient is written), parts are contiguous
+    seen = set(int(q) for q in pop.tolist() if q >= 0)
+    assert seen == set(range(J))
+    for q, p0, p1 in giant.tolist():
+        assert counts[q] > lmax and p1 - p0 == -(-int(counts[q]) // lmax)
+        assert sorted(int(part[s]) for s in range(pop.numel()) if int(pop[s]) == q) == list(range(p0, p1))
+    # group length = longest lane, groups never mix chunks
+    for g in range(ng):
+        assert int(glen[g]) == int(ln[64 * g:64 * g + 64].max())
+        assert int(base[g + 1] - base[g]) == 64 * int(glen[g])
+    for c in range(nchunks):
+        qs = [int(q) for q in pop[64 * int(cg[c]):64 * int(cg[c + 1])].tolist() if q >= 0]
+        if qs:
+            assert max(qs) < (sorted({b for b in breaks if 0 < b < J}) + [J])[c]
+
+
+@pytest.mark.skipif(not _ext.available(), reason="native extension not built")
+@pytest.mark.parametrize("J,window,lmax,breaks", [(2000, 256, 100, [500, 501, 1500]),
+                                                   (3000, 4096, 4096, []), (0, 64, 10, [])])
+def test_native_schedules_match_python(J, window, lmax, breaks):
+    counts = _counts(J, seed=1)
+    a = _ext.ext().build_lanes(counts, breaks, window, lmax)
+    b = build_lanes_py(counts, breaks, window, lmax)
+    assert all(torch.equal(x, y) for x, y in zip(a, b))
+    ta = _ext.ext().build_tiles(counts, breaks, 2048, 2048)
+    tb = build_tiles_py(counts, breaks, 2048, 2048)
+    for x, y in zip(ta[:4], tb[:4]):
+        assert torch.equal(torch.as_tensor(x), torch.as_tensor(y))
+    assert int(ta[4]) == int(tb[4])

@@ -20,6 +20,7 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--tag", default="")
     ap.add_argument("--tail", default="absolute", choices=["relative", "absolute"])
+    ap.add_argument("--layout", default="lanes", choices=["lanes", "tiles"])
     a = ap.parse_args()
     import torch
     if a.so:
@@ -31,7 +32,8 @@ def main():
     from multigrad_amd.ops import smf as S
     from multigrad_amd.ops.adam import fused_adam_
     dev = torch.device("cuda", 0)
-    data = make_population_data(a.params, a.halos, seed=1, device=dev, tail=a.tail)
+    data = make_population_data(a.params, a.halos, seed=1, device=dev, tail=a.tail,
+                                layout=a.layout)
     model = PopulationSMFModel(aux_data=data)
     model.set_target_from_truth()
     shard, bins = data["shard"], data["bins"]
@@ -57,13 +59,17 @@ def main():
         torch.cuda.synchronize()
         return e0.elapsed_time(e1) * 1e3 / a.iters
 
-    t_fwd = timeit(lambda: S.smf_forward_into(th, shard, bins, True, out, slab=slab))
+    # as in the engine step: the forward keeps the VJP residuals (lanes layout)
+    t_fwd = timeit(lambda: S.smf_forward_into(th, shard, bins, True, out, slab=slab, resid=True))
+    t_fwd_nores = timeit(lambda: S.smf_forward_into(th, shard, bins, True, out, slab=slab))
     model.engine_loss_into(out, loss, h)
-    t_vjp = timeit(lambda: S.smf_vjp_into(th, shard, bins, True, h, grad))
+    S.smf_forward_into(th, shard, bins, True, out, slab=slab, resid=True)
+    t_vjp = timeit(lambda: S.smf_vjp_into(th, shard, bins, True, h, grad, residuals_ready=True))
     t_adam = timeit(lambda: fused_adam_(u, m, v, grad, None, step, 1e-3, 0.9, 0.999, 1e-8))
-    res = {"tag": a.tag, "halos": shard.n, "params": th.numel(), "fwd_us": round(t_fwd, 1),
+    res = {"tag": a.tag, "halos": shard.n, "params": th.numel(), "layout": shard.layout,
+           "fwd_us": round(t_fwd, 1), "fwd_noresid_us": round(t_fwd_nores, 1),
            "vjp_us": round(t_vjp, 1), "adam_us": round(t_adam, 1), "fwd_blocks": nblk,
-           "ntiles": int(shard.tiles.shape[0]),
+           "ntiles": int(shard.tiles.shape[0]) if shard.layout == "tiles" else shard.ngroups,
            "fwd_Ghalo_s": round(shard.n / t_fwd / 1e3, 2), "vjp_Ghalo_s": round(shard.n / t_vjp / 1e3, 2),
            "S": [float(f"{v:.6e}") for v in out[:bins.nb].tolist()]}
     print(json.dumps(res), flush=True)
