@@ -26,7 +26,8 @@ int64_t smf_fwd_lanes_max_blocks(int64_t nb, bool log_sigma, bool rel_tail, bool
 void smf_lanes_pack(torch::Tensor xs, torch::Tensor slot_src, torch::Tensor slot_len,
                     torch::Tensor group_base, torch::Tensor group_len, torch::Tensor xi);
 void smf_forward_lanes(torch::Tensor xi, torch::Tensor slot_pop, torch::Tensor group_base,
-                       torch::Tensor group_len, torch::Tensor theta, std::vector<double> edges,
+                       torch::Tensor group_len, torch::Tensor fwd_order, torch::Tensor theta,
+                       std::vector<double> edges,
                        std::vector<double> scale, bool log_sigma, int64_t g0, int64_t g1,
                        torch::Tensor slab, int64_t nblocks, bool rel_tail,
                        c10::optional<torch::Tensor> resid);

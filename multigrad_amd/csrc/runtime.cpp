@@ -135,7 +135,8 @@ std::tuple<torch::Tensor, torch::Tensor> sort_by_population(torch::Tensor pop, i
 //          array), slot_len int32 [S], slot_part int32 [S] (partial index or -1),
 //          group_base int64 [G+1] (offset of the group in the interleaved array; the last
 //          entry is its total length), group_len int32 [G], chunk_groups int64 [C+1],
-//          giant int32 [P,3] = {pop, part_begin, part_end}, chunk_giant int64 [C+1]).
+//          giant int32 [P,3] = {pop, part_begin, part_end}, chunk_giant int64 [C+1],
+//          fwd_order int32 [G]: each chunk's groups longest first, for the forward).
 std::vector<torch::Tensor> build_lanes(torch::Tensor counts, std::vector<int64_t> breaks,
                                        int64_t window, int64_t lmax) {
   TORCH_CHECK(counts.device().is_cpu() && counts.scalar_type() == at::kLong, "counts: int64 CPU");
@@ -161,7 +162,7 @@ std::vector<torch::Tensor> build_lanes(torch::Tensor counts, std::vector<int64_t
   };
   std::vector<int32_t> slot_pop, slot_len, slot_part, giant;
   std::vector<int64_t> slot_src, group_base{0}, chunk_groups{0}, chunk_giant{0};
-  std::vector<int32_t> group_len;
+  std::vector<int32_t> group_len, fwd_order;
   std::vector<Item> items;
   int64_t nparts = 0;
   int64_t p = 0;
@@ -212,13 +213,17 @@ std::vector<torch::Tensor> build_lanes(torch::Tensor counts, std::vector<int64_t
         cglen.push_back(glen);
       }
     }
-    // Emit the chunk's groups longest first: a grid-stride over groups then hands every
-    // wavefront groups of nearly equal length in each round (static LPT balance).
+    // Groups are stored in creation (= window) order, so that the VJP's gradient writes
+    // and parameter reads of one window of populations stay together.  The forward
+    // visits them through fwd_order, longest first: a grid-stride over that order hands
+    // every wavefront groups of nearly equal length in each round (static LPT balance).
+    const int64_t gbase = (int64_t)group_len.size();
     std::vector<int64_t> order(cglen.size());
     for (size_t g = 0; g < order.size(); ++g) order[g] = (int64_t)g;
     std::stable_sort(order.begin(), order.end(),
                      [&](int64_t a, int64_t b) { return cglen[a] > cglen[b]; });
-    for (int64_t g : order) {
+    for (int64_t g : order) fwd_order.push_back((int32_t)(gbase + g));
+    for (size_t g = 0; g < cglen.size(); ++g) {
       for (int64_t l = 0; l < kLanes; ++l) {
         const Slot& sl = cslots[g * kLanes + l];
         slot_pop.push_back(sl.pop);
@@ -258,7 +263,8 @@ std::vector<torch::Tensor> build_lanes(torch::Tensor counts, std::vector<int64_t
     return t;
   };
   return {i32(slot_pop), i64(slot_src), i32(slot_len), i32(slot_part), i64(group_base),
-          i32(group_len), i64(chunk_groups), i32(giant).reshape({-1, 3}), i64(chunk_giant)};
+          i32(group_len), i64(chunk_groups), i32(giant).reshape({-1, 3}), i64(chunk_giant),
+          i32(fwd_order)};
 }
 
 }  // namespace mg

@@ -37,6 +37,7 @@ namespace mg {
 #define MG_VJP_EXP 0
 #endif
 constexpr int kMaxBins = 32;
+constexpr int kXcds = 8;  // MI355X: 8 XCDs (L2 domains), workgroups dispatched round-robin
 constexpr int kThreads = 256;
 constexpr int kItems = 8;                       // halos per thread in a tile
 constexpr int kTileHalos = kThreads * kItems;   // 2048
@@ -461,8 +462,8 @@ template <int NB, bool LOGSIG, bool REL, bool RESID>
 __global__ __launch_bounds__(kThreads, MG_LANES_MINWAVES) void smf_fwd_lanes_kernel(
     const float* __restrict__ xi, const int32_t* __restrict__ slot_pop,
     const int64_t* __restrict__ group_base, const int32_t* __restrict__ group_len,
-    const float2* __restrict__ theta, int64_t g0, int64_t g1, SmfBins bins,
-    float* __restrict__ slab, float* __restrict__ resid) {
+    const int32_t* __restrict__ fwd_order, const float2* __restrict__ theta, int64_t g0,
+    int64_t g1, SmfBins bins, float* __restrict__ slab, float* __restrict__ resid) {
   float acc[NB + 1];
   int cnt[NB + 1];
 #pragma unroll
@@ -478,23 +479,27 @@ __global__ __launch_bounds__(kThreads, MG_LANES_MINWAVES) void smf_fwd_lanes_ker
   // memory counter never makes the next group wait for those stores), and the slot ->
   // population index is fetched one group further ahead, so the dependent theta gather
   // does not wait for a load issued in the same transition.
-  int64_t g = g0 + (int64_t)blockIdx.x * (kThreads / kWave) + wid;
+  // positions k in [g0, g1) of the longest-first order; g = fwd_order[k] is the group
+  int64_t k = g0 + (int64_t)blockIdx.x * (kThreads / kWave) + wid;
+  int64_t g = 0;
   float2 th = make_float2(0.f, 0.f);
   const float* xp = xi;
   int len = 0;
   int c_next = 0;
   float xn[kLanesUnroll];
-  auto load_group = [&](int64_t gg, int c) {
+  auto load_group = [&](int64_t kk, int c) {
+    g = fwd_order[kk];
     th = theta[c < 0 ? 0 : c];
-    xp = xi + group_base[gg] + lane;
-    len = group_len[gg];
+    xp = xi + group_base[g] + lane;
+    len = group_len[g];
 #pragma unroll
     for (int u = 0; u < kLanesUnroll; ++u) xn[u] = u < len ? xp[(int64_t)u * kWave] : kLaneSentinel;
-    const int64_t ga = gg + nwaves;
-    if (ga < g1) c_next = slot_pop[ga * kWave + lane];
+    const int64_t ka = kk + nwaves;
+    if (ka < g1) c_next = slot_pop[(int64_t)fwd_order[ka] * kWave + lane];
   };
-  if (g < g1) load_group(g, slot_pop[g * kWave + lane]);
-  while (g < g1) {
+  if (k < g1) load_group(k, slot_pop[(int64_t)fwd_order[k] * kWave + lane]);
+  while (k < g1) {
+    const int64_t gc = g;
     const float ninv = -inv_sigma<LOGSIG>(th.y) * kWScale;
     const float mua = -th.x * ninv;
     float G[NB + 1], W[NB + 1];
@@ -517,17 +522,17 @@ __global__ __launch_bounds__(kThreads, MG_LANES_MINWAVES) void smf_fwd_lanes_ker
       for (int u = 0; u < kLanesUnroll; ++u)
         lane_halo<NB, LOGSIG, REL, RESID>(xc[u], ninv, mua, bins, acc, cnt, G, W);
     }
-    const int64_t gn = g + nwaves;
-    if (gn < g1) load_group(gn, c_next);
+    const int64_t kn = k + nwaves;
+    if (kn < g1) load_group(kn, c_next);
     if constexpr (RESID) {  // group-major [g][2 (NB+1)][64]: one contiguous block per group
-      float* rg = resid + g * (2 * (NB + 1) * kWave) + lane;
+      float* rg = resid + gc * (2 * (NB + 1) * kWave) + lane;
 #pragma unroll
       for (int e = 0; e <= NB; ++e) {
         rg[e * kWave] = G[e];
         rg[(NB + 1 + e) * kWave] = W[e];
       }
     }
-    g = gn;
+    k = kn;
   }
   const bool counter = lane == 0;  // the counts are per wave: fold them in once
 #pragma unroll
@@ -544,16 +549,64 @@ __global__ __launch_bounds__(kThreads, MG_LANES_MINWAVES) void smf_fwd_lanes_ker
 
 // Residual VJP over slots [s0, s1): whole populations write their gradient, parts of
 // split populations write partials[part] (summed by smf_vjp_finalize_kernel).
+#ifndef MG_VJP_LANES_PERSIST
+#define MG_VJP_LANES_PERSIST 1
+#endif
 template <int NB, bool LOGSIG>
 __global__ __launch_bounds__(kThreads) void smf_vjp_lanes_kernel(
     const int32_t* __restrict__ slot_pop, const int32_t* __restrict__ slot_part,
     const float2* __restrict__ theta, const float* __restrict__ hvec,
     const float* __restrict__ resid, int64_t s0, int64_t s1,
     float2* __restrict__ grad, float2* __restrict__ partials) {
+  constexpr int R = 2 * (NB + 1);
+  const int lane = threadIdx.x & (kWave - 1);
+#if MG_VJP_LANES_PERSIST
+  // Persistent wavefronts, one group per iteration, the next group's residuals in flight
+  // while the current one is contracted and written.  XCD-aware: workgroups are
+  // dispatched round-robin over the kXcds L2 domains, so XCD x = blockIdx % kXcds takes
+  // the x-th contiguous slice of the (window-ordered) groups -- each window's gradient
+  // lines are then fully written, and its parameter lines fetched once, in ONE L2.
+  const int64_t g0 = s0 / kWave, g1 = s1 / kWave;
+  const int xcd = blockIdx.x % kXcds;
+  const int64_t nbx = gridDim.x / kXcds;  // host launches a multiple of kXcds blocks
+  const int64_t ngx = (g1 - g0 + kXcds - 1) / kXcds;
+  const int64_t ga = g0 + xcd * ngx, gb = min(g1, ga + ngx);
+  const int64_t nw = nbx * (kThreads / kWave);
+  int64_t g = ga + (int64_t)(blockIdx.x / kXcds) * (kThreads / kWave) + (threadIdx.x >> 6);
+  float r[R];
+  int c = -1, part = -1;
+  if (g < gb) {
+#pragma unroll
+    for (int e = 0; e < R; ++e) r[e] = resid[(g * R + e) * kWave + lane];
+    c = slot_pop[g * kWave + lane];
+    part = slot_part[g * kWave + lane];
+  }
+  while (g < gb) {
+    float A = 0.0f, B = 0.0f;
+#pragma unroll
+    for (int e = 0; e <= NB; ++e) {
+      A = fmaf(hvec[e], r[e], A);
+      B = fmaf(hvec[e], r[NB + 1 + e], B);
+    }
+    const int cc = c, pp = part;
+    const int64_t gn = g + nw;
+    if (gn < gb) {
+#pragma unroll
+      for (int e = 0; e < R; ++e) r[e] = resid[(gn * R + e) * kWave + lane];
+      c = slot_pop[gn * kWave + lane];
+      part = slot_part[gn * kWave + lane];
+    }
+    if (cc >= 0) {
+      if (pp >= 0) partials[pp] = make_float2(A, B);
+      else grad[cc] = pop_grad<LOGSIG>(theta[cc], A, B);
+    }
+    g = gn;
+  }
+#else
   const int64_t s = s0 + (int64_t)blockIdx.x * kThreads + threadIdx.x;
   if (s >= s1) return;
   const int c = slot_pop[s];
-  const float* rg = resid + (s >> 6) * (2 * (NB + 1) * kWave) + (s & (kWave - 1));
+  const float* rg = resid + (s >> 6) * (R * kWave) + (s & (kWave - 1));
   float A = 0.0f, B = 0.0f;
 #pragma unroll
   for (int e = 0; e <= NB; ++e) {
@@ -564,6 +617,7 @@ __global__ __launch_bounds__(kThreads) void smf_vjp_lanes_kernel(
   const int part = slot_part[s];
   if (part >= 0) partials[part] = make_float2(A, B);
   else grad[c] = pop_grad<LOGSIG>(theta[c], A, B);
+#endif
 }
 
 // Interleave the population-sorted halos into the lanes layout (one wave per group).
@@ -817,7 +871,8 @@ void smf_lanes_pack(torch::Tensor xs, torch::Tensor slot_src, torch::Tensor slot
 
 // Forward over groups [g0, g1) of the lanes layout; optional residuals [ngroups, 2(NBP+1), 64].
 void smf_forward_lanes(torch::Tensor xi, torch::Tensor slot_pop, torch::Tensor group_base,
-                       torch::Tensor group_len, torch::Tensor theta, std::vector<double> edges,
+                       torch::Tensor group_len, torch::Tensor fwd_order, torch::Tensor theta,
+                       std::vector<double> edges,
                        std::vector<double> scale, bool log_sigma, int64_t g0, int64_t g1,
                        torch::Tensor slab, int64_t nblocks, bool rel_tail,
                        c10::optional<torch::Tensor> resid) {
@@ -825,10 +880,12 @@ void smf_forward_lanes(torch::Tensor xi, torch::Tensor slot_pop, torch::Tensor g
   check_dev(slot_pop, "slot_pop", at::kInt);
   check_dev(group_base, "group_base", at::kLong);
   check_dev(group_len, "group_len", at::kInt);
+  check_dev(fwd_order, "fwd_order", at::kInt);
   check_dev(theta, "theta", at::kFloat);
   check_dev(slab, "slab", at::kFloat);
   const int nbp = padded_bins((int)scale.size());
   const int64_t ng = group_len.numel();
+  TORCH_CHECK(fwd_order.numel() == ng, "fwd_order must list every group");
   TORCH_CHECK(g0 >= 0 && g1 <= ng && g0 <= g1, "bad group range");
   TORCH_CHECK(slot_pop.numel() == ng * kWave && group_base.numel() == ng + 1, "inconsistent lane schedule");
   TORCH_CHECK(slab.numel() >= nblocks * nbp, "slab too small");
@@ -849,7 +906,8 @@ void smf_forward_lanes(torch::Tensor xi, torch::Tensor slot_pop, torch::Tensor g
       hipLaunchKernelGGL((smf_fwd_lanes_kernel<NB, decltype(LS)::value, decltype(RT)::value, decltype(RS)::value>),
                          dim3(nblocks), dim3(kThreads), 0, stream, xi.data_ptr<float>(),
                          slot_pop.data_ptr<int32_t>(), group_base.data_ptr<int64_t>(),
-                         group_len.data_ptr<int32_t>(), tp, g0, g1, b, slab.data_ptr<float>(), rp);
+                         group_len.data_ptr<int32_t>(), fwd_order.data_ptr<int32_t>(), tp, g0, g1, b,
+                         slab.data_ptr<float>(), rp);
     }); }); });
   });
 }
@@ -880,7 +938,24 @@ void smf_vjp_lanes(torch::Tensor slot_pop, torch::Tensor slot_part, torch::Tenso
   TORCH_CHECK(s0 % kWave == 0 && s1 % kWave == 0, "slot ranges must be group aligned");
   TORCH_CHECK(resid.is_contiguous(), "resid must be contiguous");
   if (s1 > s0) {
+#if MG_VJP_LANES_PERSIST
+    static int64_t caps[kMaxBins + 1] = {0};  // per padded bin count (register use differs)
+    int64_t& cap = caps[nbp];
+    if (cap == 0) {
+      int dev = 0, occ = 0;
+      hipGetDevice(&dev);
+      hipDeviceProp_t prop;
+      hipGetDeviceProperties(&prop, dev);
+      MG_DISPATCH_NB(nbp, {
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)smf_vjp_lanes_kernel<NB, true>, kThreads, 0);
+      });
+      cap = (int64_t)std::max(1, occ) * prop.multiProcessorCount;
+    }
+    const int64_t want = (s1 - s0 + kThreads - 1) / kThreads;
+    const int64_t nblk = std::max<int64_t>(kXcds, std::min(cap, want) / kXcds * kXcds);
+#else
     const int64_t nblk = (s1 - s0 + kThreads - 1) / kThreads;
+#endif
     MG_DISPATCH_NB(nbp, {
       with_bool(log_sigma, [&](auto LS) {
         hipLaunchKernelGGL((smf_vjp_lanes_kernel<NB, decltype(LS)::value>), dim3(nblk), dim3(kThreads), 0,

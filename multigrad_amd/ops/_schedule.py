@@ -66,6 +66,7 @@ def build_lanes_py(counts, breaks, window: int, lmax: int):
     group_base, group_len = [0], []
     chunk_groups, chunk_giant = [0], [0]
     giant = []
+    fwd_order = []
     part_begin = {}
     nparts = 0
     p = 0
@@ -95,8 +96,9 @@ def build_lanes_py(counts, breaks, window: int, lmax: int):
                     else:
                         slots.append((-1, 0, 0, -1))
                 cgroups.append((max(sl[1] for sl in slots), slots))
-        cgroups.sort(key=lambda g: -g[0])  # longest groups first (stable)
-        for glen, slots in cgroups:
+        gbase = len(group_len)
+        fwd_order += [gbase + k for k in sorted(range(len(cgroups)), key=lambda k: -cgroups[k][0])]
+        for glen, slots in cgroups:  # stored in window order; the forward goes longest first
             for q, n, src, part in slots:
                 slot_pop.append(q)
                 slot_len.append(n)
@@ -111,4 +113,4 @@ def build_lanes_py(counts, breaks, window: int, lmax: int):
     i64 = lambda v: torch.tensor(v, dtype=torch.int64)  # noqa: E731
     g = torch.tensor(giant, dtype=torch.int32).reshape(-1, 3)
     return [i32(slot_pop), i64(slot_src), i32(slot_len), i32(slot_part), i64(group_base),
-            i32(group_len), i64(chunk_groups), g, i64(chunk_giant)]
+            i32(group_len), i64(chunk_groups), g, i64(chunk_giant), i32(fwd_order)]

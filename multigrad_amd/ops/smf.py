@@ -202,7 +202,7 @@ class PopulationShard:
         except ImportError:
             out = build_lanes_py(self.counts, pb[1:-1], self._lane_window, self._lane_lmax)
         (slot_pop, slot_src, slot_len, slot_part, group_base, group_len, chunk_groups, giant,
-         chunk_giant) = out
+         chunk_giant, fwd_order) = out
         dev = self.device
         self.nslots = int(slot_pop.numel())
         self.ngroups = int(group_len.numel())
@@ -212,6 +212,7 @@ class PopulationShard:
         self.slot_part = slot_part.to(dev)
         self.group_base = group_base.to(dev)
         self.group_len = group_len.to(dev)
+        self.fwd_order = fwd_order.to(dev)
         self.giant = giant.to(dev).contiguous()
         nparts = int(giant[:, 2].max()) if giant.numel() else 0
         self.partials = torch.zeros(max(nparts, 1) * 2, dtype=torch.float32, device=dev)
@@ -302,7 +303,7 @@ def smf_forward_slab(theta: torch.Tensor, shard: PopulationShard, bins: SmfBins,
         g0, g1 = shard.group_range(chunk)
         rbuf = shard.resid_buffer(bins.nbp) if resid else None
         ext().smf_forward_lanes(shard.xi, shard.slot_pop, shard.group_base, shard.group_len,
-                                theta, list(bins.edges), list(bins.scale), bool(log_sigma),
+                                shard.fwd_order, theta, list(bins.edges), list(bins.scale), bool(log_sigma),
                                 g0, g1, slab, nblk, bins.rel_tail, rbuf)
         if resid:
             shard.resid_epoch += 1

@@ -23,7 +23,8 @@ def _counts(J, seed=0):
                                                    (0, 64, 10, [])])
 def test_lanes_schedule_invariants(J, window, lmax, breaks):
     counts = _counts(J)
-    (pop, src, ln, part, base, glen, cg, giant, cgi) = build_lanes_py(counts, breaks, window, lmax)
+    (pop, src, ln, part, base, glen, cg, giant, cgi, ford) = build_lanes_py(counts, breaks, window,
+                                                                          lmax)
     nchunks = len(sorted({b for b in breaks if 0 < b < J})) + 1
     assert len(cg) == nchunks + 1 and len(cgi) == nchunks + 1
     ng = glen.numel()
@@ -47,6 +48,17 @@ def test_lanes_schedule_invariants(J, window, lmax, breaks):
     for q, p0, p1 in giant.tolist():
         assert counts[q] > lmax and p1 - p0 == -(-int(counts[q]) // lmax)
         assert sorted(int(part[s]) for s in range(pop.numel()) if int(pop[s]) == q) == list(range(p0, p1))
+    # groups are stored in window order; the forward order is a per-chunk permutation,
+    # longest group first
+    starts = [0] + sorted({b for b in breaks if 0 < b < J})
+    for c in range(len(cg) - 1):
+        a, b = int(cg[c]), int(cg[c + 1])
+        assert sorted(ford[a:b].tolist()) == list(range(a, b))
+        lens = glen[ford[a:b].long()]
+        assert (lens[:-1] >= lens[1:]).all()
+        firsts = [int(pop[64 * g]) for g in range(a, b) if int(pop[64 * g]) >= 0]
+        wins = [(q - starts[c]) // window for q in firsts]
+        assert wins == sorted(wins)
     # group length = longest lane, groups never mix chunks
     for g in range(ng):
         assert int(glen[g]) == int(ln[64 * g:64 * g + 64].max())
