@@ -53,7 +53,8 @@ build_tiles(torch::Tensor counts, std::vector<int64_t> breaks, int64_t tile_halo
             int64_t tile_pops);
 std::tuple<torch::Tensor, torch::Tensor> sort_by_population(torch::Tensor pop, int64_t npop);
 std::vector<torch::Tensor> build_lanes(torch::Tensor counts, std::vector<int64_t> breaks,
-                                       int64_t window, int64_t lmax);
+                                       int64_t window, int64_t lmax,
+                                       c10::optional<torch::Tensor> order_counts);
 }  // namespace mg
 
 PYBIND11_MODULE(_C, m) {
@@ -75,5 +76,6 @@ PYBIND11_MODULE(_C, m) {
   m.def("lincomb", &mg::lincomb);
   m.def("build_tiles", &mg::build_tiles);
   m.def("sort_by_population", &mg::sort_by_population);
-  m.def("build_lanes", &mg::build_lanes);
+  m.def("build_lanes", &mg::build_lanes, pybind11::arg("counts"), pybind11::arg("breaks"),
+        pybind11::arg("window"), pybind11::arg("lmax"), pybind11::arg("order_counts") = pybind11::none());
 }

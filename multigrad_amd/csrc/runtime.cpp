@@ -136,15 +136,27 @@ std::tuple<torch::Tensor, torch::Tensor> sort_by_population(torch::Tensor pop, i
 //          group_base int64 [G+1] (offset of the group in the interleaved array; the last
 //          entry is its total length), group_len int32 [G], chunk_groups int64 [C+1],
 //          giant int32 [P,3] = {pop, part_begin, part_end}, chunk_giant int64 [C+1],
-//          fwd_order int32 [G]: each chunk's groups longest first, for the forward).
+//          fwd_order int32 [G]: each chunk's groups longest first, for the forward,
+//          slot_pidx int32 [S]: internal parameter-unit index per slot (-1: empty),
+//          perm int32 [J]: internal unit index -> population).
+// order_counts (optional, int64 [J]): counts that decide the population order inside a
+// window (default: counts); pass the cross-rank sums so that all ranks agree on it.
 std::vector<torch::Tensor> build_lanes(torch::Tensor counts, std::vector<int64_t> breaks,
-                                       int64_t window, int64_t lmax) {
+                                       int64_t window, int64_t lmax,
+                                       c10::optional<torch::Tensor> order_counts) {
   TORCH_CHECK(counts.device().is_cpu() && counts.scalar_type() == at::kLong, "counts: int64 CPU");
   TORCH_CHECK(window >= 1 && lmax >= 1, "bad lane-schedule limits");
   constexpr int64_t kLanes = 64;
   auto c = counts.contiguous();
   const int64_t* cnt = c.data_ptr<int64_t>();
   const int64_t J = c.numel();
+  torch::Tensor oc = c;
+  if (order_counts.has_value() && order_counts->defined()) {
+    oc = order_counts->contiguous();
+    TORCH_CHECK(oc.device().is_cpu() && oc.scalar_type() == at::kLong && oc.numel() == J,
+                "order_counts: int64 CPU [J]");
+  }
+  const int64_t* key = oc.data_ptr<int64_t>();
   std::vector<int64_t> brk;
   for (auto b : breaks)
     if (b > 0 && b < J) brk.push_back(b);
@@ -158,7 +170,7 @@ std::vector<torch::Tensor> build_lanes(torch::Tensor counts, std::vector<int64_t
     off[p + 1] = off[p] + cnt[p];
   }
   struct Item {
-    int64_t len, pop, part, src;
+    int64_t key, len, pop, part, src;
   };
   std::vector<int32_t> slot_pop, slot_len, slot_part, giant;
   std::vector<int64_t> slot_src, group_base{0}, chunk_groups{0}, chunk_giant{0};
@@ -185,16 +197,18 @@ std::vector<torch::Tensor> build_lanes(torch::Tensor counts, std::vector<int64_t
         if (n > lmax) {
           const int64_t k = (n + lmax - 1) / lmax;
           for (int64_t i = 0; i < k; ++i)
-            items.push_back({std::min(lmax, n - i * lmax), q, i, off[q] + i * lmax});
+            items.push_back({key[q], std::min(lmax, n - i * lmax), q, i, off[q] + i * lmax});
           // partial indices are contiguous per split population, in population order
           giant.insert(giant.end(), {(int32_t)q, (int32_t)nparts, (int32_t)(nparts + k)});
           nparts += k;
         } else {
-          items.push_back({n, q, -1, off[q]});
+          items.push_back({key[q], n, q, -1, off[q]});
         }
       }
+      // order by the *ordering* counts (the global ones under data parallelism, so every
+      // rank derives the same population order), lengths are the local counts
       std::stable_sort(items.begin(), items.end(), [](const Item& a, const Item& b) {
-        return a.len > b.len;
+        return a.key > b.key;
       });
       const size_t n_items = items.size();
       const size_t padded = (n_items + kLanes - 1) / kLanes * kLanes;
@@ -252,6 +266,22 @@ std::vector<torch::Tensor> build_lanes(torch::Tensor counts, std::vector<int64_t
       }
     }
   }
+  // Internal parameter order: populations by first appearance in (window-ordered) slot
+  // order.  Lanes of a group then hold consecutive internal indices, so parameter reads
+  // and gradient writes in internal order are coalesced; with global ordering counts the
+  // order is identical on every rank.
+  std::vector<int32_t> slot_pidx(slot_pop.size(), -1), perm, pidx_of(J, -1);
+  perm.reserve(J);
+  for (size_t s2 = 0; s2 < slot_pop.size(); ++s2) {
+    const int32_t q = slot_pop[s2];
+    if (q < 0) continue;
+    if (pidx_of[q] < 0) {
+      pidx_of[q] = (int32_t)perm.size();
+      perm.push_back(q);
+    }
+    slot_pidx[s2] = pidx_of[q];
+  }
+  TORCH_CHECK((int64_t)perm.size() == J, "every population needs a slot");
   auto i32 = [](const std::vector<int32_t>& v) {
     auto t = torch::empty({(int64_t)v.size()}, torch::kInt);
     if (!v.empty()) std::memcpy(t.data_ptr<int32_t>(), v.data(), v.size() * sizeof(int32_t));
@@ -264,7 +294,7 @@ std::vector<torch::Tensor> build_lanes(torch::Tensor counts, std::vector<int64_t
   };
   return {i32(slot_pop), i64(slot_src), i32(slot_len), i32(slot_part), i64(group_base),
           i32(group_len), i64(chunk_groups), i32(giant).reshape({-1, 3}), i64(chunk_giant),
-          i32(fwd_order)};
+          i32(fwd_order), i32(slot_pidx), i32(perm)};
 }
 
 }  // namespace mg

@@ -31,7 +31,8 @@ Engine protocol (implemented by :class:`~multigrad_amd.models.population.Populat
 ``engine_units() -> (J, params_per_unit)``, ``engine_set_chunks(unit_bounds)``,
 ``engine_nS()``, ``engine_fwd_rows(chunk)``, ``engine_forward_chunk(theta, slab, chunk)
 -> rows``, ``engine_reduce(slab, rows, S)``, ``engine_loss_into(S, loss, h)``,
-``engine_vjp_into(theta, h, grad, chunk)``.  Every method works on CPU tensors too
+``engine_vjp_into(theta, h, grad, chunk)``, optionally ``engine_param_perm()`` (the
+unit order the model wants the engine vectors in).  Every method works on CPU tensors too
 (PyTorch reference math), which is how the multi-rank orchestration is tested on gloo.
 """
 from __future__ import annotations
@@ -124,6 +125,19 @@ class FusedAdamEngine:
         W = self.size if self.zero else 1
         ub, pb, P_pad, lengths = plan_chunks(J, upp, W, self.nchunks_req)
         md.engine_set_chunks(ub)
+        # Internal order: models may keep the engine vectors in their own unit order
+        # (e.g. the lanes layout's slot order, for coalesced parameter/gradient access).
+        # It must keep every chunk's units inside the chunk, and be the same on all ranks;
+        # user-facing values (guess, bounds, params, trajectory) are permuted at the edge.
+        perm = getattr(md, "engine_param_perm", lambda: None)()
+        if perm is not None:
+            perm = torch.as_tensor(perm, device=dev).to(torch.int64)
+            ar = torch.arange(upp, device=dev, dtype=torch.int64)
+            self.pidx = (perm[:, None] * upp + ar).reshape(-1)     # internal -> user index
+            self.inv_pidx = torch.empty_like(self.pidx)
+            self.inv_pidx[self.pidx] = torch.arange(P, device=dev)  # user -> internal index
+        else:
+            self.pidx = self.inv_pidx = None
         self.P, self.P_pad, self.pb, self.lengths = P, P_pad, pb, lengths
         self.C = len(lengths)
         self.lr, self.b1, self.b2, self.eps = float(learning_rate), float(b1), float(b2), float(eps)
@@ -132,6 +146,11 @@ class FusedAdamEngine:
         assert p0.numel() == P, f"guess has {p0.numel()} params, model expects {P}"
         f32 = dict(dtype=torch.float32, device=dev)
         bounds = Bounds.from_spec(param_bounds, P, device=dev)
+        if self.pidx is not None:
+            p0 = p0[self.pidx]
+            if bounds is not None:
+                bounds = Bounds(bounds.lo[self.pidx].contiguous(), bounds.hi[self.pidx].contiguous(),
+                                bounds.kind[self.pidx].contiguous())
         if bounds is not None and P_pad > P:
             pad = P_pad - P
             bounds = Bounds(torch.cat([bounds.lo, torch.full((pad,), -math.inf, **f32)]),
@@ -300,11 +319,17 @@ class FusedAdamEngine:
             self.drain()
             self.history.record(self.step_host - 1, self.theta[:self.P])
 
+    def to_user(self, t: torch.Tensor) -> torch.Tensor:
+        """Engine (internal) parameter order -> the model's parameter order (last dim)."""
+        if self.pidx is None:
+            return t
+        return t[..., self.inv_pidx]
+
     def trajectory(self) -> torch.Tensor:
         """The recorded parameter trajectory (assembled across ranks under ZeRO)."""
         self.drain()
         if self.traj_loc is None:
-            return self.history.result()
+            return self.to_user(self.history.result())
         W = self.size
         nloc = self.traj_loc.shape[1]
         rows = self.step_host + 1
@@ -317,11 +342,11 @@ class FusedAdamEngine:
             for r in range(W):
                 a = self.pb[c] + r * n
                 out[:, a:a + n] = gathered[r, :, o:o + n]
-        return out[:, :self.P]
+        return self.to_user(out[:, :self.P])
 
     def params(self) -> torch.Tensor:
         self.drain()
-        return self.theta[:self.P]
+        return self.to_user(self.theta[:self.P])
 
     def last_loss(self) -> float:
         return float(self.loss.item())
@@ -407,6 +432,7 @@ class _EngineObjective:
         return float(e.loss.double().item()), g
 
     def full(self, x: torch.Tensor) -> torch.Tensor:
+        """The full parameter vector (model order) for the optimizer's vector x."""
         self._load(x)
         self.e.drain()
-        return self.e.theta[:self.e.P].clone()
+        return self.e.to_user(self.e.theta[:self.e.P]).clone()

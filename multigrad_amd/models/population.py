@@ -79,7 +79,7 @@ def make_population_data(num_params: int = 10_000_000, num_halos: int = 1 << 27,
     logm = (10.0 - torch.log10(1.0 - q)).to(torch.float32)          # log10(1e10/(1-q))
     del idx, q
     shard = PopulationShard(logm, pop.to(torch.int32), npop, device=device, chunks=chunks,
-                            layout=layout)
+                            layout=layout, comm=comm)
     del logm, pop
     cidx = torch.arange(npop, dtype=torch.int64, device=device)
     truth = torch.empty(2 * npop, dtype=torch.float32, device=device)
@@ -151,6 +151,14 @@ class PopulationSMFModel(OnePointModel):
     def engine_set_chunks(self, unit_bounds):
         self.shard.set_chunks(unit_bounds)
 
+    def engine_param_perm(self):
+        """Internal unit order of the engine vectors (lanes layout: populations in slot
+        order, so parameter reads and gradient writes are coalesced), or None."""
+        return self.shard.perm if self.shard.layout == "lanes" else None
+
+    def _engine_order(self) -> str:
+        return "internal" if self.shard.layout == "lanes" else "user"
+
     def engine_nS(self) -> int:
         return self.bins.nbp
 
@@ -164,7 +172,8 @@ class PopulationSMFModel(OnePointModel):
     def engine_forward_chunk(self, theta, slab, chunk=None) -> int:
         # the engine always runs the VJP of a chunk after this forward at the same theta,
         # so the forward stores the VJP residuals (lanes layout)
-        return smf_forward_slab(theta, self.shard, self.bins, True, slab, chunk, resid=True)
+        return smf_forward_slab(theta, self.shard, self.bins, True, slab, chunk, resid=True,
+                                order=self._engine_order())
 
     def engine_reduce(self, slab, nrows, S):
         return smf_slab_reduce(slab, nrows, self.bins, S)
@@ -188,8 +197,9 @@ class PopulationSMFModel(OnePointModel):
 
     def engine_vjp_into(self, theta, h, grad, chunk=None):
         return smf_vjp_into(theta, self.shard, self.bins, True, h, grad, chunk=chunk,
-                            residuals_ready=True)
+                            residuals_ready=True, order=self._engine_order())
 
     # simple (unchunked) protocol helpers
     def engine_partial_into(self, theta, out, slab=None, chunk=None):
-        return smf_forward_into(theta, self.shard, self.bins, True, out, slab=slab, chunk=chunk)
+        return smf_forward_into(theta, self.shard, self.bins, True, out, slab=slab, chunk=chunk,
+                                order=self._engine_order())

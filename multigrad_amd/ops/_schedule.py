@@ -54,10 +54,12 @@ def build_tiles_py(counts, breaks, tile_halos: int, tile_pops: int):
     return t, g, torch.tensor(chunk_tiles), torch.tensor(chunk_giant), nslots
 
 
-def build_lanes_py(counts, breaks, window: int, lmax: int):
+def build_lanes_py(counts, breaks, window: int, lmax: int, order_counts=None):
     """Mirror of ``csrc/runtime.cpp:build_lanes`` (lanes layout schedule); same outputs."""
     lanes = 64
     cnt = np.asarray(torch.as_tensor(counts).cpu().numpy(), dtype=np.int64)
+    key = cnt if order_counts is None else \
+        np.asarray(torch.as_tensor(order_counts).cpu().numpy(), dtype=np.int64)
     J = cnt.size
     brk = sorted({int(b) for b in breaks if 0 < int(b) < J}) + [J]
     off = np.zeros(J + 1, dtype=np.int64)
@@ -79,19 +81,20 @@ def build_lanes_py(counts, breaks, window: int, lmax: int):
                 n = int(cnt[q])
                 if n > lmax:
                     k = -(-n // lmax)
-                    items += [(min(lmax, n - i * lmax), q, i, int(off[q]) + i * lmax) for i in range(k)]
+                    items += [(int(key[q]), min(lmax, n - i * lmax), q, i, int(off[q]) + i * lmax)
+                              for i in range(k)]
                     giant.append((q, nparts, nparts + k))
                     part_begin[q] = nparts
                     nparts += k
                 else:
-                    items.append((n, q, -1, int(off[q])))
+                    items.append((int(key[q]), n, q, -1, int(off[q])))
             items.sort(key=lambda it: -it[0])  # stable: ties keep population/part order
             padded = -(-len(items) // lanes) * lanes
             for i in range(0, padded, lanes):
                 slots = []
                 for l in range(lanes):
                     if i + l < len(items):
-                        n, q, part, src = items[i + l]
+                        _, n, q, part, src = items[i + l]
                         slots.append((q, n, src, part_begin[q] + part if part >= 0 else -1))
                     else:
                         slots.append((-1, 0, 0, -1))
@@ -109,8 +112,17 @@ def build_lanes_py(counts, breaks, window: int, lmax: int):
         p = pend
         chunk_groups.append(len(group_len))
         chunk_giant.append(len(giant))
+    pidx_of = {}
+    perm, slot_pidx = [], []
+    for q in slot_pop:
+        if q >= 0 and q not in pidx_of:
+            pidx_of[q] = len(perm)
+            perm.append(q)
+        slot_pidx.append(pidx_of[q] if q >= 0 else -1)
+    assert len(perm) == J, "every population needs a slot"
     i32 = lambda v: torch.tensor(v, dtype=torch.int32)  # noqa: E731
     i64 = lambda v: torch.tensor(v, dtype=torch.int64)  # noqa: E731
     g = torch.tensor(giant, dtype=torch.int32).reshape(-1, 3)
     return [i32(slot_pop), i64(slot_src), i32(slot_len), i32(slot_part), i64(group_base),
-            i32(group_len), i64(chunk_groups), g, i64(chunk_giant), i32(fwd_order)]
+            i32(group_len), i64(chunk_groups), g, i64(chunk_giant), i32(fwd_order),
+            i32(slot_pidx), i32(perm)]

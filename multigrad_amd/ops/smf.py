@@ -125,13 +125,17 @@ class PopulationShard:
     def __init__(self, x, pop=None, npop: int = 1, device=None, chunks: int = 1,
                  tile_halos: int = TILE_HALOS, tile_pops: int = TILE_POPS,
                  layout: str = "lanes", lane_window: int = LANE_WINDOW,
-                 lane_lmax: int = LANE_LMAX):
+                 lane_lmax: int = LANE_LMAX, comm=None):
         x = torch.as_tensor(x)
         device = torch.device(device) if device is not None else x.device
         self.device = device
         if layout not in ("lanes", "tiles"):
             raise ValueError("layout must be 'lanes' or 'tiles'")
-        self.layout = layout if (pop is not None and device.type == "cuda") else "tiles"
+        # lanes on the CPU builds the schedule and the internal parameter order only (the
+        # math runs through the PyTorch reference), which is how the engine's internal
+        # ordering is exercised by the multi-rank CPU tests
+        self.layout = layout if pop is not None else "tiles"
+        self._comm = comm
         self._lane_window, self._lane_lmax = int(lane_window), int(lane_lmax)
         self.resid = None          # lanes: [ngroups, 2 (nbp+1), 64] residuals of the last forward
         self.resid_epoch = 0       # bumped by every residual-writing forward
@@ -159,6 +163,13 @@ class PopulationShard:
             xs = xs.contiguous()
         self.x = xs
         self.counts = counts
+        # the lanes population order must be identical on every rank of a data-parallel
+        # job: it is decided by the cross-rank sums of the counts
+        self.order_counts = None
+        if self.layout == "lanes" and comm is not None and comm.size > 1:
+            oc = counts.clone().to(torch.int64)
+            comm.all_reduce(oc)
+            self.order_counts = oc
         self.offsets = torch.zeros(self.npop + 1, dtype=torch.int64)
         self.offsets[1:] = torch.cumsum(counts, 0)
         self._tile_halos, self._tile_pops = tile_halos, tile_pops
@@ -198,11 +209,12 @@ class PopulationShard:
         from ._schedule import build_lanes_py
         try:
             out = ext().build_lanes(self.counts.to(torch.int64), list(pb[1:-1]),
-                                    self._lane_window, self._lane_lmax)
+                                    self._lane_window, self._lane_lmax, self.order_counts)
         except ImportError:
-            out = build_lanes_py(self.counts, pb[1:-1], self._lane_window, self._lane_lmax)
+            out = build_lanes_py(self.counts, pb[1:-1], self._lane_window, self._lane_lmax,
+                                 self.order_counts)
         (slot_pop, slot_src, slot_len, slot_part, group_base, group_len, chunk_groups, giant,
-         chunk_giant, fwd_order) = out
+         chunk_giant, fwd_order, slot_pidx, perm) = out
         dev = self.device
         self.nslots = int(slot_pop.numel())
         self.ngroups = int(group_len.numel())
@@ -214,11 +226,23 @@ class PopulationShard:
         self.group_len = group_len.to(dev)
         self.fwd_order = fwd_order.to(dev)
         self.giant = giant.to(dev).contiguous()
+        # internal parameter order (see build_lanes): perm[i] = population of unit i
+        self.slot_pidx = slot_pidx.to(dev)
+        self.perm = perm.to(torch.int64).to(dev)
+        self.inv_perm = torch.empty_like(self.perm)
+        self.inv_perm[self.perm] = torch.arange(self.npop, device=dev)
+        gi = giant.clone()
+        if gi.numel():
+            gi[:, 0] = self.inv_perm.cpu()[gi[:, 0].long()].to(torch.int32)
+        self.giant_int = gi.to(dev).contiguous()
         nparts = int(giant[:, 2].max()) if giant.numel() else 0
         self.partials = torch.zeros(max(nparts, 1) * 2, dtype=torch.float32, device=dev)
-        self.xi = torch.empty(int(group_base[-1]), dtype=torch.float32, device=dev)
-        ext().smf_lanes_pack(self.x, slot_src.to(dev), slot_len.to(dev), self.group_base,
-                             self.group_len, self.xi)
+        if dev.type == "cuda":
+            self.xi = torch.empty(int(group_base[-1]), dtype=torch.float32, device=dev)
+            ext().smf_lanes_pack(self.x, slot_src.to(dev), slot_len.to(dev), self.group_base,
+                                 self.group_len, self.xi)
+        else:
+            self.xi = None
         self.resid = None
         self.resid_epoch += 1
 
@@ -228,6 +252,14 @@ class PopulationShard:
         if self.resid is None or tuple(self.resid.shape) != shape:
             self.resid = torch.empty(shape, dtype=torch.float32, device=self.device)
         return self.resid
+
+    def slot_index(self, order: str) -> torch.Tensor:
+        """Slot -> parameter unit index for ``order`` in {"user", "internal"}."""
+        return self.slot_pidx if order == "internal" else self.slot_pop
+
+    def to_user_units(self, t: torch.Tensor) -> torch.Tensor:
+        """(J, k) rows in internal order -> user (population) order."""
+        return t[self.inv_perm]
 
     def group_range(self, chunk: Optional[int] = None):
         if chunk is None:
@@ -244,6 +276,8 @@ class PopulationShard:
         """Forward grid: enough 256-thread workgroups for the halos (tiles layout) or for
         the 64-slot groups (lanes layout, one per wavefront), capped at one fully
         resident wave of workgroups."""
+        if self.device.type != "cuda":
+            return 1
         if self.layout == "lanes":
             g0, g1 = self.group_range(chunk)
             key = ("lanes", nbins, bool(log_sigma), bool(rel_tail))
@@ -283,17 +317,32 @@ def _build_tiles(counts, breaks, tile_halos, tile_pops):
 
 
 # ---------------------------------------------------------------------------- device ops
+def _user_theta(theta: torch.Tensor, shard: PopulationShard, order: str) -> torch.Tensor:
+    """Parameters in population (user) order, from ``order`` (CPU reference paths)."""
+    if order != "internal":
+        return theta
+    t = theta.reshape(-1)[:2 * shard.npop].reshape(-1, 2)
+    return shard.to_user_units(t).reshape(-1)
+
+
 def smf_forward_slab(theta: torch.Tensor, shard: PopulationShard, bins: SmfBins, log_sigma: bool,
-                     slab: torch.Tensor, chunk: Optional[int] = None, resid: bool = False) -> int:
+                     slab: torch.Tensor, chunk: Optional[int] = None, resid: bool = False,
+                     order: str = "user") -> int:
     """Forward of the shard (or one population chunk) into per-workgroup slab rows;
     returns the number of rows written.  CPU: one row from the PyTorch reference.
-    ``resid`` (lanes layout): also store the VJP residuals of these populations."""
+    ``resid`` (lanes layout): also store the VJP residuals of these populations.
+    ``order="internal"`` (lanes layout): ``theta`` is in the shard's internal parameter
+    order (``shard.perm``), the order the fused engine keeps its vectors in; chunks are
+    the same population ranges in either order."""
+    if order == "internal" and shard.layout != "lanes":
+        raise ValueError("internal parameter order needs the lanes layout")
     h0, h1 = shard.halo_range(chunk)
     if theta.device.type != "cuda":
         with torch.no_grad():
             xs = shard.x[h0:h1]
             ps = None if shard.pop is None else shard.pop[h0:h1]
-            row = smf_sumstats_reference(theta.reshape(-1).float(), xs, ps, bins, log_sigma)
+            th = _user_theta(theta, shard, order)
+            row = smf_sumstats_reference(th.reshape(-1).float(), xs, ps, bins, log_sigma)
             sc = torch.as_tensor(bins.scale, dtype=row.dtype)
         slab[:bins.nbp].zero_()
         slab[:bins.nb] = (row / sc).to(slab.dtype)  # unscaled bin sums (scale at reduce)
@@ -302,9 +351,10 @@ def smf_forward_slab(theta: torch.Tensor, shard: PopulationShard, bins: SmfBins,
     if shard.layout == "lanes":
         g0, g1 = shard.group_range(chunk)
         rbuf = shard.resid_buffer(bins.nbp) if resid else None
-        ext().smf_forward_lanes(shard.xi, shard.slot_pop, shard.group_base, shard.group_len,
-                                shard.fwd_order, theta, list(bins.edges), list(bins.scale), bool(log_sigma),
-                                g0, g1, slab, nblk, bins.rel_tail, rbuf)
+        ext().smf_forward_lanes(shard.xi, shard.slot_index(order), shard.group_base,
+                                shard.group_len, shard.fwd_order, theta, list(bins.edges),
+                                list(bins.scale), bool(log_sigma), g0, g1, slab, nblk,
+                                bins.rel_tail, rbuf)
         if resid:
             shard.resid_epoch += 1
         return nblk
@@ -327,30 +377,35 @@ def smf_slab_reduce(slab: torch.Tensor, nrows: int, bins: SmfBins, out: torch.Te
 
 def smf_forward_into(theta: torch.Tensor, shard: PopulationShard, bins: SmfBins, log_sigma: bool,
                      out: torch.Tensor, slab: Optional[torch.Tensor] = None,
-                     chunk: Optional[int] = None, resid: bool = False) -> torch.Tensor:
+                     chunk: Optional[int] = None, resid: bool = False,
+                     order: str = "user") -> torch.Tensor:
     """Partial sumstats of the shard (or one population chunk) into ``out[:nbp]``."""
     if slab is None:
         h0, h1 = shard.halo_range(chunk)
         nblk = shard.fwd_blocks(max(h1 - h0, 1), bins.nb, log_sigma, bins.rel_tail, chunk)
         slab = torch.empty(nblk * bins.nbp, dtype=torch.float32, device=theta.device)
-    nrows = smf_forward_slab(theta, shard, bins, log_sigma, slab, chunk, resid)
+    nrows = smf_forward_slab(theta, shard, bins, log_sigma, slab, chunk, resid, order)
     return smf_slab_reduce(slab, nrows, bins, out)
 
 
 def smf_vjp_into(theta: torch.Tensor, shard: PopulationShard, bins: SmfBins, log_sigma: bool,
                  h: torch.Tensor, grad: torch.Tensor, chunk: Optional[int] = None,
-                 residuals_ready: bool = False) -> torch.Tensor:
+                 residuals_ready: bool = False, order: str = "user") -> torch.Tensor:
     """Per-population VJP with edge weights ``h`` into ``grad`` (the chunk's parameters
     only).  CPU: autograd of the PyTorch reference restricted to the chunk's halos.
 
     Lanes layout: the VJP reads the residuals of a forward at the same ``theta``.  Pass
     ``residuals_ready=True`` only when the caller has just run
     ``smf_forward_*(..., resid=True)`` at this ``theta`` for this chunk (the fused engine
-    does); otherwise the residual forward is recomputed here first."""
+    does); otherwise the residual forward is recomputed here first.  ``order`` as in
+    :func:`smf_forward_slab` (``grad`` is written in the same order as ``theta``)."""
+    if order == "internal" and shard.layout != "lanes":
+        raise ValueError("internal parameter order needs the lanes layout")
     if theta.device.type != "cuda":
         h0, h1 = shard.halo_range(chunk)
         p0, p1 = (0, shard.npop) if chunk is None else (shard.chunk_pops[chunk], shard.chunk_pops[chunk + 1])
-        th = theta.detach().reshape(-1)[:2 * shard.npop].double().clone().requires_grad_(True)
+        th = _user_theta(theta.detach(), shard, order)
+        th = th.reshape(-1)[:2 * shard.npop].double().clone().requires_grad_(True)
         xs = shard.x[h0:h1].double()
         ps = None if shard.pop is None else shard.pop[h0:h1]
         hw = h[:bins.nb + 1].double() * math.sqrt(2 * math.pi)
@@ -365,6 +420,8 @@ def smf_vjp_into(theta: torch.Tensor, shard: PopulationShard, bins: SmfBins, log
             (g,) = torch.autograd.grad(f, th, allow_unused=True)
         if g is None:
             g = torch.zeros_like(th)
+        if order == "internal":  # internal units [p0, p1) are populations perm[p0:p1]
+            g = g.reshape(-1, 2)[shard.perm].reshape(-1)
         grad.reshape(-1)[2 * p0:2 * p1] = g[2 * p0:2 * p1].to(grad.dtype)
         return grad
     E = ext()
@@ -372,13 +429,14 @@ def smf_vjp_into(theta: torch.Tensor, shard: PopulationShard, bins: SmfBins, log
         if not residuals_ready or shard.resid is None:
             nblk = shard.fwd_blocks(1, bins.nb, log_sigma, bins.rel_tail, chunk)
             slab = torch.empty(nblk * bins.nbp, dtype=torch.float32, device=theta.device)
-            smf_forward_slab(theta, shard, bins, log_sigma, slab, chunk, resid=True)
+            smf_forward_slab(theta, shard, bins, log_sigma, slab, chunk, resid=True, order=order)
         g0, g1 = shard.group_range(chunk)
         k0, k1 = (0, shard.giant.shape[0]) if chunk is None else \
             (shard.chunk_giant[chunk], shard.chunk_giant[chunk + 1])
-        E.smf_vjp_lanes(shard.slot_pop, shard.slot_part, theta, h, shard.resid_buffer(bins.nbp),
-                        64 * g0, 64 * g1, list(bins.scale), bool(log_sigma), grad,
-                        shard.partials, shard.giant[k0:k1])
+        giant = shard.giant_int if order == "internal" else shard.giant
+        E.smf_vjp_lanes(shard.slot_index(order), shard.slot_part, theta, h,
+                        shard.resid_buffer(bins.nbp), 64 * g0, 64 * g1, list(bins.scale),
+                        bool(log_sigma), grad, shard.partials, giant[k0:k1])
         return grad
     if chunk is None:
         t0, t1 = 0, shard.tiles.shape[0]

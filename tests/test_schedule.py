@@ -23,8 +23,8 @@ def _counts(J, seed=0):
                                                    (0, 64, 10, [])])
 def test_lanes_schedule_invariants(J, window, lmax, breaks):
     counts = _counts(J)
-    (pop, src, ln, part, base, glen, cg, giant, cgi, ford) = build_lanes_py(counts, breaks, window,
-                                                                          lmax)
+    (pop, src, ln, part, base, glen, cg, giant, cgi, ford, spidx, perm) = build_lanes_py(
+        counts, breaks, window, lmax)
     nchunks = len(sorted({b for b in breaks if 0 < b < J})) + 1
     assert len(cg) == nchunks + 1 and len(cgi) == nchunks + 1
     ng = glen.numel()
@@ -59,6 +59,18 @@ def test_lanes_schedule_invariants(J, window, lmax, breaks):
         firsts = [int(pop[64 * g]) for g in range(a, b) if int(pop[64 * g]) >= 0]
         wins = [(q - starts[c]) // window for q in firsts]
         assert wins == sorted(wins)
+    # internal order: a permutation of the populations, chunk-aligned, and consistent with
+    # the slots (first appearance order)
+    assert sorted(perm.tolist()) == list(range(J))
+    for s_ in range(pop.numel()):
+        if int(pop[s_]) >= 0:
+            assert int(perm[int(spidx[s_])]) == int(pop[s_])
+        else:
+            assert int(spidx[s_]) == -1
+    bounds = [0] + sorted({b for b in breaks if 0 < b < J}) + [J]
+    for c in range(len(bounds) - 1):
+        chunk = perm[bounds[c]:bounds[c + 1]].tolist()
+        assert all(bounds[c] <= q < bounds[c + 1] for q in chunk)
     # group length = longest lane, groups never mix chunks
     for g in range(ng):
         assert int(glen[g]) == int(ln[64 * g:64 * g + 64].max())
@@ -77,8 +89,26 @@ def test_native_schedules_match_python(J, window, lmax, breaks):
     a = _ext.ext().build_lanes(counts, breaks, window, lmax)
     b = build_lanes_py(counts, breaks, window, lmax)
     assert all(torch.equal(x, y) for x, y in zip(a, b))
+    glob = counts * 3 + torch.arange(J) % 5  # e.g. cross-rank sums
+    a = _ext.ext().build_lanes(counts, breaks, window, lmax, glob)
+    b = build_lanes_py(counts, breaks, window, lmax, glob)
+    assert all(torch.equal(x, y) for x, y in zip(a, b))
     ta = _ext.ext().build_tiles(counts, breaks, 2048, 2048)
     tb = build_tiles_py(counts, breaks, 2048, 2048)
     for x, y in zip(ta[:4], tb[:4]):
         assert torch.equal(torch.as_tensor(x), torch.as_tensor(y))
     assert int(ta[4]) == int(tb[4])
+
+
+def test_internal_order_is_rank_independent():
+    """Two ranks with different local counts but the same ordering (global) counts get
+    the same internal parameter order."""
+    rng = np.random.default_rng(4)
+    J = 3000
+    l0 = torch.tensor(rng.poisson(14, J), dtype=torch.int64)
+    l1 = torch.tensor(rng.poisson(14, J), dtype=torch.int64)
+    l1[7] = 9000  # split into parts on one rank only
+    glob = l0 + l1
+    p0 = build_lanes_py(l0, [1000], 256, 4096, glob)[-1]
+    p1 = build_lanes_py(l1, [1000], 256, 4096, glob)[-1]
+    assert torch.equal(p0, p1)
