@@ -112,4 +112,40 @@ __device__ __forceinline__ void normal_tail_parts_w(float w, float& p, float& g)
   g = fast_exp2(-w * w);
 }
 
+// Two halos at once (packed fp32: v_pk_fma/v_pk_mul do both lanes of a pair in one
+// issue, the transcendental and bitwise steps stay per element).  Same contract as
+// normal_tail_parts_w.
+typedef float v2f __attribute__((ext_vector_type(2)));
+
+template <bool REL>
+__device__ __forceinline__ void normal_tail_parts_w2(v2f w, v2f& p, v2f& g) {
+  v2f r;
+  if constexpr (REL) {
+    constexpr float kK = 0x1.99999ap+1f;
+    r.x = fast_rcp(fabsf(w.x) + kK);
+    r.y = fast_rcp(fabsf(w.y) + kK);
+    p = (v2f)(-0x1.c816e0p+7f);
+    p = p * r + 0x1.9741fcp+7f;
+    p = p * r + -0x1.42955cp+4f;
+    p = p * r + 0x1.d3aa86p+3f;
+    p = p * r + 0x1.5e9730p+1f;
+    p = p * r + 0x1.1b7a3ap+0f;
+    p = p * r + 0x1.5a604cp-2f;
+    p = p * r + 0x1.7dececp-18f;
+  } else {
+    constexpr float kK = 0x1.ccccccp+0f;
+    r.x = fast_rcp(fabsf(w.x) + kK);
+    r.y = fast_rcp(fabsf(w.y) + kK);
+    p = (v2f)(0x1.3a12c0p+0f);
+    p = p * r + -0x1.bacb20p+1f;
+    p = p * r + 0x1.901deap+1f;
+    p = p * r + -0x1.0b406ap-7f;
+    p = p * r + 0x1.b317b2p-2f;
+    p = p * r + -0x1.428b48p-8f;
+  }
+  const v2f t = -w * w;
+  g.x = fast_exp2(t.x);
+  g.y = fast_exp2(t.y);
+}
+
 }  // namespace mg

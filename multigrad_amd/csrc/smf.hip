@@ -450,6 +450,44 @@ __device__ __forceinline__ void lane_halo(float x, float ninv, float mua, const 
   }
 }
 
+// Two halos of one lane in packed fp32 (see normal_tail_parts_w2): acc2 keeps one
+// partial per halo slot of the pair; the residual sums are shared.
+template <int NB, bool LOGSIG, bool REL, bool RESID>
+__device__ __forceinline__ void lane_halo2(v2f x, float ninv, float mua, const SmfBins& b,
+                                           v2f (&acc2)[NB + 1], int (&cnt)[NB + 1],
+                                           float (&G)[NB + 1], float (&W)[NB + 1]) {
+  const v2f mu = x * (-ninv) + mua;
+#pragma unroll
+  for (int e = 0; e <= NB; ++e) {
+    const v2f n = (v2f)(b.edge[e]) * ninv + mu;
+    v2f p, g;
+    normal_tail_parts_w2<REL>(n, p, g);
+    v2f sg;
+    sg.x = __builtin_copysignf(g.x, n.x);
+    sg.y = __builtin_copysignf(g.y, n.y);
+#if MG_LANES_ACC2
+    acc2[e] = p * sg + acc2[e];
+#else
+    acc2[e].x = fmaf(p.y, sg.y, fmaf(p.x, sg.x, acc2[e].x));
+#endif
+    cnt[e] += __builtin_popcountll(__builtin_amdgcn_ballot_w64(n.x < 0.0f)) +
+              __builtin_popcountll(__builtin_amdgcn_ballot_w64(n.y < 0.0f));
+    if constexpr (RESID) {
+      G[e] += g.x + g.y;
+      W[e] = fmaf(-g.y, n.y, fmaf(-g.x, n.x, W[e]));
+    }
+  }
+}
+
+// Packed two-halo path: 10% fewer VALU cycles per halo pair, but it needs 108 VGPRs
+// (4 waves/SIMD) to avoid spills; measured on MI355X it ties the scalar path (690 vs
+// 692 us at 1.34e8 halos), so the scalar path at 6 waves/SIMD stays the default.
+#ifndef MG_LANES_V2
+#define MG_LANES_V2 0
+#endif
+#ifndef MG_LANES_ACC2
+#define MG_LANES_ACC2 0  // 1: one bin partial per halo of the pair (more registers)
+#endif
 #ifndef MG_LANES_MINWAVES
 #define MG_LANES_MINWAVES 6
 #endif
@@ -471,6 +509,11 @@ __global__ __launch_bounds__(kThreads, MG_LANES_MINWAVES) void smf_fwd_lanes_ker
     acc[k] = 0.0f;
     cnt[k] = 0;
   }
+#if MG_LANES_V2
+  v2f acc2[NB + 1];
+#pragma unroll
+  for (int k = 0; k <= NB; ++k) acc2[k] = (v2f)(0.0f);
+#endif
   const int lane = threadIdx.x & (kWave - 1);
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t nwaves = (int64_t)gridDim.x * (kThreads / kWave);
@@ -518,9 +561,20 @@ __global__ __launch_bounds__(kThreads, MG_LANES_MINWAVES) void smf_fwd_lanes_ker
         const int jn = j + kLanesUnroll + u;
         xn[u] = jn < len ? xp[(int64_t)jn * kWave] : kLaneSentinel;
       }
+#if MG_LANES_V2
+      static_assert(kLanesUnroll % 2 == 0, "packed path takes halo pairs");
+#pragma unroll
+      for (int u = 0; u < kLanesUnroll; u += 2) {
+        v2f xv;
+        xv.x = xc[u];
+        xv.y = xc[u + 1];
+        lane_halo2<NB, LOGSIG, REL, RESID>(xv, ninv, mua, bins, acc2, cnt, G, W);
+      }
+#else
 #pragma unroll
       for (int u = 0; u < kLanesUnroll; ++u)
         lane_halo<NB, LOGSIG, REL, RESID>(xc[u], ninv, mua, bins, acc, cnt, G, W);
+#endif
     }
     const int64_t kn = k + nwaves;
     if (kn < g1) load_group(kn, c_next);
@@ -534,6 +588,10 @@ __global__ __launch_bounds__(kThreads, MG_LANES_MINWAVES) void smf_fwd_lanes_ker
     }
     k = kn;
   }
+#if MG_LANES_V2
+#pragma unroll
+  for (int k = 0; k <= NB; ++k) acc[k] = acc2[k].x + acc2[k].y;
+#endif
   const bool counter = lane == 0;  // the counts are per wave: fold them in once
 #pragma unroll
   for (int k = 0; k < NB; ++k)
