@@ -117,13 +117,31 @@ __device__ __forceinline__ void normal_tail_parts_w(float w, float& p, float& g)
 // normal_tail_parts_w.
 typedef float v2f __attribute__((ext_vector_type(2)));
 
+// PAIR_RCP: the two reciprocals share one v_rcp (1/a = b/(ab), 1/b = a/(ab)); both
+// factors are >= K, so ab only overflows for the lane sentinel (|w| ~ 1e30), where the
+// reciprocal becomes 0 and the Gaussian factor 0 keeps the contribution exactly zero.
+#ifndef MG_PAIR_RCP
+#define MG_PAIR_RCP 0
+#endif
+__device__ __forceinline__ v2f pair_rcp(float a, float b) {
+  v2f r;
+#if MG_PAIR_RCP
+  const float R = fast_rcp(a * b);
+  r.x = R * b;
+  r.y = R * a;
+#else
+  r.x = fast_rcp(a);
+  r.y = fast_rcp(b);
+#endif
+  return r;
+}
+
 template <bool REL>
 __device__ __forceinline__ void normal_tail_parts_w2(v2f w, v2f& p, v2f& g) {
   v2f r;
   if constexpr (REL) {
     constexpr float kK = 0x1.99999ap+1f;
-    r.x = fast_rcp(fabsf(w.x) + kK);
-    r.y = fast_rcp(fabsf(w.y) + kK);
+    r = pair_rcp(fabsf(w.x) + kK, fabsf(w.y) + kK);
     p = (v2f)(-0x1.c816e0p+7f);
     p = p * r + 0x1.9741fcp+7f;
     p = p * r + -0x1.42955cp+4f;
@@ -134,8 +152,7 @@ __device__ __forceinline__ void normal_tail_parts_w2(v2f w, v2f& p, v2f& g) {
     p = p * r + 0x1.7dececp-18f;
   } else {
     constexpr float kK = 0x1.ccccccp+0f;
-    r.x = fast_rcp(fabsf(w.x) + kK);
-    r.y = fast_rcp(fabsf(w.y) + kK);
+    r = pair_rcp(fabsf(w.x) + kK, fabsf(w.y) + kK);
     p = (v2f)(0x1.3a12c0p+0f);
     p = p * r + -0x1.bacb20p+1f;
     p = p * r + 0x1.901deap+1f;

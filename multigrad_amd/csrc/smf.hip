@@ -479,6 +479,79 @@ __device__ __forceinline__ void lane_halo2(v2f x, float ninv, float mua, const S
   }
 }
 
+// Edge-pair packing: the NB+1 edges of ONE halo are evaluated two at a time in packed
+// fp32 (v_pk_fma / v_pk_mul / v_pk_add on (edge 2i, edge 2i+1)), so every per-edge sum --
+// the signed-tail accumulator and the two residual sums -- is itself a register pair and
+// accumulates with one packed instruction, with no cross-lane shuffles or moves.  With an
+// odd edge count the last edge of the two halos of an unrolled pair forms the remaining
+// pair (its accumulators keep one partial per halo, folded once at the end).
+// Packed per pair: the edge fma, w^2, the Horner chain, the accumulate and both residual
+// updates; per element: |w|+K, v_rcp, v_exp, the sign (v_bfi) and the count compare.
+template <int NB>
+struct EdgePairs {
+  static constexpr int NE = NB + 1;
+  static constexpr int NP = NE / 2;             // pairs inside one halo
+  static constexpr int NX = NE & 1;             // 1: cross-halo pair for the last edge
+  static constexpr int NV = NP + NX;            // accumulator pairs
+};
+
+template <int NB, bool REL, bool RESID>
+__device__ __forceinline__ void ep_eval(v2f n, v2f (&acc)[EdgePairs<NB>::NV],
+                                        v2f (&G)[EdgePairs<NB>::NV], v2f (&W)[EdgePairs<NB>::NV],
+                                        int i, int& ca, int& cb) {
+  v2f p, g;
+  normal_tail_parts_w2<REL>(n, p, g);
+  v2f sg;
+  sg.x = __builtin_copysignf(g.x, n.x);
+  sg.y = __builtin_copysignf(g.y, n.y);
+  acc[i] = p * sg + acc[i];
+  ca += __builtin_popcountll(__builtin_amdgcn_ballot_w64(n.x < 0.0f));
+  cb += __builtin_popcountll(__builtin_amdgcn_ballot_w64(n.y < 0.0f));
+  if constexpr (RESID) {
+    G[i] = G[i] + g;
+    W[i] = (-g) * n + W[i];
+  }
+}
+
+template <int NB, bool LOGSIG, bool REL, bool RESID>
+__device__ __forceinline__ void lane_halo_ep(float x0, float x1, float ninv, float mua,
+                                             const SmfBins& b,
+                                             v2f (&acc)[EdgePairs<NB>::NV], int (&cnt)[NB + 1],
+                                             v2f (&G)[EdgePairs<NB>::NV],
+                                             v2f (&W)[EdgePairs<NB>::NV]) {
+  using E = EdgePairs<NB>;
+  const float mu0 = fmaf(x0, -ninv, mua);
+  const float mu1 = fmaf(x1, -ninv, mua);
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const float mu = h ? mu1 : mu0;
+#pragma unroll
+    for (int i = 0; i < E::NP; ++i) {
+      v2f e2;
+      e2.x = b.edge[2 * i];
+      e2.y = b.edge[2 * i + 1];
+      const v2f n = e2 * ninv + mu;
+      ep_eval<NB, REL, RESID>(n, acc, G, W, i, cnt[2 * i], cnt[2 * i + 1]);
+    }
+  }
+  if constexpr (E::NX) {
+    v2f m2;
+    m2.x = mu0;
+    m2.y = mu1;
+    const v2f n = (v2f)(b.edge[E::NE - 1] * ninv) + m2;
+    int c2 = 0;
+    ep_eval<NB, REL, RESID>(n, acc, G, W, E::NP, cnt[E::NE - 1], c2);
+    cnt[E::NE - 1] += c2;
+  }
+}
+
+// Measured on MI355X (1e7 params, 1.34e8 halos, internal order, with residuals): the
+// edge-pair path at 4 waves/SIMD (118 VGPRs, no spills) 595 us vs 615-624 us for the
+// compiler-packed scalar path at 6 waves; at 5 or 6 waves the edge-pair path spills.
+#ifndef MG_LANES_EP
+#define MG_LANES_EP 1
+#endif
+
 // Packed two-halo path: 10% fewer VALU cycles per halo pair, but it needs 108 VGPRs
 // (4 waves/SIMD) to avoid spills; measured on MI355X it ties the scalar path (690 vs
 // 692 us at 1.34e8 halos), so the scalar path at 6 waves/SIMD stays the default.
@@ -489,12 +562,49 @@ __device__ __forceinline__ void lane_halo2(v2f x, float ninv, float mua, const S
 #define MG_LANES_ACC2 0  // 1: one bin partial per halo of the pair (more registers)
 #endif
 #ifndef MG_LANES_MINWAVES
-#define MG_LANES_MINWAVES 6
+#define MG_LANES_MINWAVES (MG_LANES_EP ? 4 : 6)
 #endif
 #ifndef MG_LANES_UNROLL
 #define MG_LANES_UNROLL 2
 #endif
 constexpr int kLanesUnroll = MG_LANES_UNROLL;
+
+// Halo j of a lane (sentinel past the end).  MG_LANES_UNCOND: the load itself is
+// unconditional (the host pads xi by 16 rows) and the value is selected, so there is no
+// branch around it and the compiler can count the outstanding loads exactly
+// (s_waitcnt vmcnt(N) instead of vmcnt(0) at every loop back-edge).
+#ifndef MG_LANES_UNCOND
+#define MG_LANES_UNCOND 0
+#endif
+// (the select happens at the use, lane_use, so the wait lands there and not at the load)
+__device__ __forceinline__ float lane_load(const float* xp, int j, int len) {
+#if MG_LANES_UNCOND
+  return xp[(int64_t)j * kWave];
+#else
+  return j < len ? xp[(int64_t)j * kWave] : kLaneSentinel;
+#endif
+}
+__device__ __forceinline__ float lane_use(float v, int j, int len) {
+#if MG_LANES_UNCOND
+  return j < len ? v : kLaneSentinel;
+#else
+  return v;
+#endif
+}
+
+// Residual stores: MG_LANES_NTSTORE writes them non-temporal (streamed past the caches).
+#ifndef MG_LANES_NTSTORE
+#define MG_LANES_NTSTORE 0
+#endif
+__device__ __forceinline__ void resid_store(float* p, float v) {
+#if defined(MG_DBG_NOSTORE)  // timing experiments only: keeps the sums live, drops the stores
+  if (v == 12345.678f) *p = v;
+#elif MG_LANES_NTSTORE
+  __builtin_nontemporal_store(v, p);
+#else
+  *p = v;
+#endif
+}
 
 template <int NB, bool LOGSIG, bool REL, bool RESID>
 __global__ __launch_bounds__(kThreads, MG_LANES_MINWAVES) void smf_fwd_lanes_kernel(
@@ -509,7 +619,13 @@ __global__ __launch_bounds__(kThreads, MG_LANES_MINWAVES) void smf_fwd_lanes_ker
     acc[k] = 0.0f;
     cnt[k] = 0;
   }
-#if MG_LANES_V2
+#if MG_LANES_EP
+  using EP = EdgePairs<NB>;
+  static_assert(kLanesUnroll % 2 == 0, "edge-pair path takes halos two at a time");
+  v2f accp[EP::NV];
+#pragma unroll
+  for (int k = 0; k < EP::NV; ++k) accp[k] = (v2f)(0.0f);
+#elif MG_LANES_V2
   v2f acc2[NB + 1];
 #pragma unroll
   for (int k = 0; k <= NB; ++k) acc2[k] = (v2f)(0.0f);
@@ -536,7 +652,7 @@ __global__ __launch_bounds__(kThreads, MG_LANES_MINWAVES) void smf_fwd_lanes_ker
     xp = xi + group_base[g] + lane;
     len = group_len[g];
 #pragma unroll
-    for (int u = 0; u < kLanesUnroll; ++u) xn[u] = u < len ? xp[(int64_t)u * kWave] : kLaneSentinel;
+    for (int u = 0; u < kLanesUnroll; ++u) xn[u] = lane_load(xp, u, len);
     const int64_t ka = kk + nwaves;
     if (ka < g1) c_next = slot_pop[(int64_t)fwd_order[ka] * kWave + lane];
   };
@@ -545,23 +661,36 @@ __global__ __launch_bounds__(kThreads, MG_LANES_MINWAVES) void smf_fwd_lanes_ker
     const int64_t gc = g;
     const float ninv = -inv_sigma<LOGSIG>(th.y) * kWScale;
     const float mua = -th.x * ninv;
+#if MG_LANES_EP
+    v2f Gp[EP::NV], Wp[EP::NV];
+#pragma unroll
+    for (int e = 0; e < EP::NV; ++e) {
+      Gp[e] = (v2f)(0.0f);
+      Wp[e] = (v2f)(0.0f);
+    }
+#else
     float G[NB + 1], W[NB + 1];
 #pragma unroll
     for (int e = 0; e <= NB; ++e) {
       G[e] = 0.0f;
       W[e] = 0.0f;
     }
+#endif
     // the next kLanesUnroll loads are in flight while the current halos are computed;
     // past-the-end halos are the sentinel (exact zero contribution)
     for (int j = 0; j < len; j += kLanesUnroll) {
       float xc[kLanesUnroll];
 #pragma unroll
       for (int u = 0; u < kLanesUnroll; ++u) {
-        xc[u] = xn[u];
+        xc[u] = lane_use(xn[u], j + u, len);
         const int jn = j + kLanesUnroll + u;
-        xn[u] = jn < len ? xp[(int64_t)jn * kWave] : kLaneSentinel;
+        xn[u] = lane_load(xp, jn, len);
       }
-#if MG_LANES_V2
+#if MG_LANES_EP
+#pragma unroll
+      for (int u = 0; u < kLanesUnroll; u += 2)
+        lane_halo_ep<NB, LOGSIG, REL, RESID>(xc[u], xc[u + 1], ninv, mua, bins, accp, cnt, Gp, Wp);
+#elif MG_LANES_V2
       static_assert(kLanesUnroll % 2 == 0, "packed path takes halo pairs");
 #pragma unroll
       for (int u = 0; u < kLanesUnroll; u += 2) {
@@ -580,15 +709,36 @@ __global__ __launch_bounds__(kThreads, MG_LANES_MINWAVES) void smf_fwd_lanes_ker
     if (kn < g1) load_group(kn, c_next);
     if constexpr (RESID) {  // group-major [g][2 (NB+1)][64]: one contiguous block per group
       float* rg = resid + gc * (2 * (NB + 1) * kWave) + lane;
+#if MG_LANES_EP
+      float G[NB + 1], W[NB + 1];
+#pragma unroll
+      for (int i = 0; i < EP::NP; ++i) {
+        G[2 * i] = Gp[i].x;
+        G[2 * i + 1] = Gp[i].y;
+        W[2 * i] = Wp[i].x;
+        W[2 * i + 1] = Wp[i].y;
+      }
+      if constexpr (EP::NX) {
+        G[NB] = Gp[EP::NP].x + Gp[EP::NP].y;
+        W[NB] = Wp[EP::NP].x + Wp[EP::NP].y;
+      }
+#endif
 #pragma unroll
       for (int e = 0; e <= NB; ++e) {
-        rg[e * kWave] = G[e];
-        rg[(NB + 1 + e) * kWave] = W[e];
+        resid_store(rg + e * kWave, G[e]);
+        resid_store(rg + (NB + 1 + e) * kWave, W[e]);
       }
     }
     k = kn;
   }
-#if MG_LANES_V2
+#if MG_LANES_EP
+#pragma unroll
+  for (int i = 0; i < EP::NP; ++i) {
+    acc[2 * i] = accp[i].x;
+    acc[2 * i + 1] = accp[i].y;
+  }
+  if constexpr (EP::NX) acc[NB] = accp[EP::NP].x + accp[EP::NP].y;
+#elif MG_LANES_V2
 #pragma unroll
   for (int k = 0; k <= NB; ++k) acc[k] = acc2[k].x + acc2[k].y;
 #endif

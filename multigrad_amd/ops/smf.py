@@ -238,7 +238,10 @@ class PopulationShard:
         nparts = int(giant[:, 2].max()) if giant.numel() else 0
         self.partials = torch.zeros(max(nparts, 1) * 2, dtype=torch.float32, device=dev)
         if dev.type == "cuda":
-            self.xi = torch.empty(int(group_base[-1]), dtype=torch.float32, device=dev)
+            # tail padding: the forward's prefetch loads run up to 2*unroll+1 rows past a
+            # group's end unconditionally (values masked), so the last group stays in bounds
+            self.xi = torch.full((int(group_base[-1]) + 64 * 16,), -1e30, dtype=torch.float32,
+                                 device=dev)
             ext().smf_lanes_pack(self.x, slot_src.to(dev), slot_len.to(dev), self.group_base,
                                  self.group_len, self.xi)
         else:

@@ -65,20 +65,23 @@ def main():
     model.engine_loss_into(out, loss, h)
     S.smf_forward_into(th, shard, bins, True, out, slab=slab, resid=True)
     t_vjp = timeit(lambda: S.smf_vjp_into(th, shard, bins, True, h, grad, residuals_ready=True))
-    t_vjp_int = None
+    t_vjp_int = t_fwd_int = None
     if shard.layout == "lanes":  # the engine's internal (slot) parameter order
         thi = th.reshape(-1, 2)[shard.perm].reshape(-1).contiguous()
         S.smf_forward_into(thi, shard, bins, True, out, slab=slab, resid=True, order="internal")
+        t_fwd_int = round(timeit(lambda: S.smf_forward_into(thi, shard, bins, True, out, slab=slab,
+                                                            resid=True, order="internal")), 1)
         t_vjp_int = round(timeit(lambda: S.smf_vjp_into(thi, shard, bins, True, h, grad,
                                                         residuals_ready=True,
                                                         order="internal")), 1)
     t_adam = timeit(lambda: fused_adam_(u, m, v, grad, None, step, 1e-3, 0.9, 0.999, 1e-8))
     res = {"tag": a.tag, "halos": shard.n, "params": th.numel(), "layout": shard.layout,
            "fwd_us": round(t_fwd, 1), "fwd_noresid_us": round(t_fwd_nores, 1),
-           "vjp_us": round(t_vjp, 1), "vjp_internal_us": t_vjp_int, "adam_us": round(t_adam, 1), "fwd_blocks": nblk,
+           "vjp_us": round(t_vjp, 1), "vjp_internal_us": t_vjp_int, "fwd_internal_us": t_fwd_int, "adam_us": round(t_adam, 1), "fwd_blocks": nblk,
            "ntiles": int(shard.tiles.shape[0]) if shard.layout == "tiles" else shard.ngroups,
            "fwd_Ghalo_s": round(shard.n / t_fwd / 1e3, 2), "vjp_Ghalo_s": round(shard.n / t_vjp / 1e3, 2),
-           "S": [float(f"{v:.6e}") for v in out[:bins.nb].tolist()]}
+           "S": [float(f"{v:.7e}") for v in out[:bins.nb].tolist()],
+           "grad_l1": float(f"{grad.double().abs().sum().item():.9e}")}
     print(json.dumps(res), flush=True)
 
 
