@@ -39,6 +39,11 @@ def main(argv=None):
                     help="global number of halos (fixed across GPU counts: strong scaling)")
     ap.add_argument("--lr", type=float, default=1e-3)
     ap.add_argument("--history", default="full", help="trajectory: full | last | <stride>")
+    ap.add_argument("--placement", default="owner", choices=["owner", "hashed"],
+                    help="halo -> rank placement for N > 1: 'owner' splits the catalog by "
+                         "population (gradient shards complete on their owner, no gradient "
+                         "collective); 'hashed' splits it by halo index (dense gradient, "
+                         "ZeRO reduce-scatter + all-gather every step)")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--profile-phases", action="store_true")
     args = ap.parse_args(argv)
@@ -57,7 +62,8 @@ def main(argv=None):
     dev = torch.device("cuda", torch.cuda.current_device())
 
     t_setup = time.perf_counter()
-    data = make_population_data(args.params, args.halos, seed=1234, comm=comm, device=dev)
+    data = make_population_data(args.params, args.halos, seed=1234, comm=comm, device=dev,
+                                placement=args.placement if comm.size > 1 else "hashed")
     model = PopulationSMFModel(aux_data=data, comm=comm)
     model.set_target_from_truth()
     history = args.history if args.history in ("full", "last") else int(args.history)
@@ -105,13 +111,19 @@ def main(argv=None):
                      f"({args.params // 2} populations x (a, log10 sigma)), 10 bins, log-MSE",
             "global_batch": args.halos,
             "seq_len": 10,
-            "parallelism": f"dp{comm.size}",
+            "parallelism": f"dp{comm.size}" + ("-owner" if engine.owner else ""),
             "params": args.params,
             "halos_global": args.halos,
             "optimizer": "Adam (fused HIP kernel), full trajectory" if history == "full"
                          else f"Adam (fused HIP kernel), history={history}",
             "graph": bool(engine.use_graph),
-            "optimizer_sharding": "zero1" if engine.zero else "replicated",
+            "optimizer_sharding": ("owner" if engine.owner else "zero1" if engine.zero
+                                   else "replicated"),
+            "placement": data["placement"],
+            "grad_collective": ("none: owner-local gradients, sumstat all-reduce only"
+                                if engine.owner else "RCCL reduce-scatter + all-gather"
+                                if engine.zero else "RCCL all-reduce" if comm.size > 1
+                                else "none (1 rank)"),
             "chunks": engine.C,
         },
         "loss_first_timed": loss0,

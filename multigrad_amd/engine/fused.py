@@ -22,6 +22,19 @@ RS + AG move exactly the bytes of one all-reduce, but the optimizer work and the
 state drop to 1/W per GPU and every collective hides behind compute of a neighbouring
 chunk.  Parameters stay bitwise identical across ranks (each slice has one owner).
 
+Owner mode (world > 1, model data placed by parameter ownership): when the model
+reports unit bounds ``engine_owner_units() -> [W+1]`` and every rank's data touches only
+units inside its own range (``engine_support_units()``, verified collectively at setup),
+the chunks ARE the ranks' ranges.  Rank r's gradient on its range is then complete
+locally and zero elsewhere, so the step is
+
+    forward(own chunk) -> all-reduce(S) -> loss -> VJP(own chunk) -> Adam(own chunk)
+
+with the K-float sumstat all-reduce as the only collective: the dense P-float
+gradient reduction of data parallelism (reference multigrad/multigrad.py:531-532)
+is provably all zeros outside the owner's range and is not sent.  Parameters, moments and
+trajectory are sharded by owner and assembled on request.
+
 On a single GPU the whole step is captured once into a HIP graph and replayed; the
 device step counter inside the Adam kernel makes the replay self-advancing.  This
 replaces the reference's per-step host round trips (4 host crossings per
@@ -87,6 +100,8 @@ class FusedAdamEngine:
         for more than one rank (``MULTIGRAD_ZERO``)
     chunks : number of parameter chunks for collective/compute overlap (default 1 on a
         single rank, 4 otherwise; ``MULTIGRAD_CHUNKS``)
+    owner : owner mode (see the module docstring): default whenever the model's data
+        placement allows it on more than one rank (``MULTIGRAD_OWNER``)
 
     With ZeRO the parameter all-gathers run on a second communicator (its own RCCL
     stream), so the all-gather of chunk c overlaps the reduce-scatter of chunk c+1
@@ -96,13 +111,20 @@ class FusedAdamEngine:
     """
 
     def __init__(self, model, comm=None, graph: Optional[bool] = None,
-                 zero: Optional[bool] = None, chunks: Optional[int] = None):
+                 zero: Optional[bool] = None, chunks: Optional[int] = None,
+                 owner: Optional[bool] = None):
         self.model = model
         self.comm = model.comm if comm is None else comm
         self.size = 1 if self.comm is None else self.comm.size
         self.rank = 0 if self.comm is None else self.comm.rank
         z = _env_flag("MULTIGRAD_ZERO", zero)
         self.zero = (self.size > 1) if z is None else bool(z) and self.size > 1
+        # owner mode: None = whenever the model's placement allows it on >1 rank; True =
+        # also on a single rank (exercises the owner schedule); False = never
+        o = _env_flag("MULTIGRAD_OWNER", owner)
+        self.allow_owner = True if o is None else bool(o)
+        self.force_owner = bool(o)
+        self.owner = False
         nc = chunks if chunks is not None else int(os.environ.get("MULTIGRAD_CHUNKS", "0")) or None
         self.nchunks_req = nc if nc is not None else (1 if self.size == 1 else 4)
         self.comm_ag = None  # second communicator (own RCCL stream) for parameter all-gathers
@@ -122,8 +144,16 @@ class FusedAdamEngine:
             self.use_graph = False
         J, upp = md.engine_units()
         P = J * upp
-        W = self.size if self.zero else 1
-        ub, pb, P_pad, lengths = plan_chunks(J, upp, W, self.nchunks_req)
+        owner_ub = self._owner_units(md, J)
+        self.owner = owner_ub is not None
+        if self.owner:
+            ub = owner_ub
+            pb = [u * upp for u in ub]
+            P_pad = P
+            lengths = [pb[i + 1] - pb[i] for i in range(len(pb) - 1)]
+        else:
+            W = self.size if self.zero else 1
+            ub, pb, P_pad, lengths = plan_chunks(J, upp, W, self.nchunks_req)
         md.engine_set_chunks(ub)
         # Internal order: models may keep the engine vectors in their own unit order
         # (e.g. the lanes layout's slot order, for coalesced parameter/gradient access).
@@ -172,7 +202,20 @@ class FusedAdamEngine:
         self.h = torch.zeros(nS + 1, **f32)
         self.loss = torch.zeros(1, **f32)
         self.step_dev = torch.zeros((self.C, 2), dtype=torch.int32, device=dev)
-        if self.zero:
+        if self.owner:
+            a, b = pb[self.rank], pb[self.rank + 1]
+            self.own_range = (a, b)
+            n = b - a
+            self.m = torch.zeros(n, **f32)
+            self.v = torch.zeros(n, **f32)
+            if bounds is not None:
+                self.bounds_loc = Bounds(bounds.lo[a:b].contiguous(), bounds.hi[a:b].contiguous(),
+                                         bounds.kind[a:b].contiguous())
+                self.u_loc = self.bounds_loc.forward(theta[a:b]).contiguous()
+            else:
+                self.bounds_loc = None
+                self.u_loc = None
+        elif self.zero:
             self.loc_len = [L // W for L in lengths]
             self.loc_off = [sum(self.loc_len[:c]) for c in range(self.C)]
             nloc = sum(self.loc_len)
@@ -195,11 +238,17 @@ class FusedAdamEngine:
             self.v = torch.zeros(P_pad, **f32)
         self.step_host = 0
         self.nsteps = int(nsteps)
-        self.history = History(history if not (self.zero and history == "full") else "last",
+        sharded = self.zero or self.owner
+        self.history = History(history if not (sharded and history == "full") else "last",
                                nsteps, theta[:P].detach().clone())
         self.traj_loc = None
         self.history_mode = history
-        if self.zero:
+        if self.owner:
+            if history == "full":
+                a, b = self.own_range
+                self.traj_loc = torch.zeros((self.nsteps + 1, b - a), **f32)
+                self.traj_loc[0] = theta[a:b]
+        elif self.zero:
             if history == "full":
                 self.traj_loc = torch.zeros((self.nsteps + 1, sum(self.loc_len)), **f32)
                 for c in range(self.C):
@@ -214,6 +263,38 @@ class FusedAdamEngine:
         return self
 
     # ------------------------------------------------------------------ helpers
+    def _owner_units(self, md, J):
+        """Owner-mode unit bounds if the model's data placement allows it on every rank."""
+        if not self.allow_owner or (self.size == 1 and not self.force_owner):
+            return None
+        fn = getattr(md, "engine_owner_units", None)
+        ub = fn() if fn is not None else None
+        if ub is None and self.size == 1 and self.force_owner:
+            ub = [0, J]
+        ok = ub is not None and len(ub) == self.size + 1 and ub[0] == 0 and ub[-1] == J \
+            and all(x <= y for x, y in zip(ub, ub[1:]))
+        if ok:
+            lo, hi = md.engine_support_units()
+            ok = hi <= lo or (ub[self.rank] <= lo and hi <= ub[self.rank + 1])
+        flag = torch.tensor([1 if ok else 0], dtype=torch.int64)
+        self.comm.all_reduce(flag, op="min")
+        return [int(u) for u in ub] if int(flag[0]) == 1 else None
+
+    def _assemble(self, own: torch.Tensor) -> torch.Tensor:
+        """Owner mode: the full (model-order) vector(s) from every rank's owned slices;
+        ``own`` is ``[..., n_own]`` (identical leading shape on all ranks)."""
+        lead = tuple(own.shape[:-1])
+        L = max(self.lengths)
+        buf = torch.zeros(lead + (L,), dtype=own.dtype, device=self.device)
+        buf[..., :own.shape[-1]] = own
+        gathered = torch.empty((self.size,) + lead + (L,), dtype=own.dtype, device=self.device)
+        self.comm.all_gather_into_tensor(gathered.reshape(-1), buf.reshape(-1))
+        out = torch.empty(lead + (self.P,), dtype=own.dtype, device=self.device)
+        for r in range(self.size):
+            a, b = self.pb[r], self.pb[r + 1]
+            out[..., a:b] = gathered[r][..., :b - a]
+        return out
+
     def _bslice(self, c):
         if self.bounds_loc is None:
             return None
@@ -237,7 +318,7 @@ class FusedAdamEngine:
     def _forward_loss(self):
         md = self.model
         row = 0
-        for c in range(self.C):
+        for c in ([self.rank] if self.owner else range(self.C)):
             self._drain(c)
             n = md.engine_forward_chunk(self.theta, self.slab[row * self.nS:], c)
             row += n
@@ -250,7 +331,17 @@ class FusedAdamEngine:
         md = self.model
         self._forward_loss()
         hb = self.history.buf.reshape(-1) if self.history.mode == "full" else None
-        if self.zero:
+        if self.owner:
+            c = self.rank
+            md.engine_vjp_into(self.theta, self.h, self.grad, chunk=c)
+            a, b = self.own_range
+            u = self.u_loc if self.u_loc is not None else self.theta[a:b]
+            p = self.theta[a:b] if self.u_loc is not None else None
+            tb = None if self.traj_loc is None else self.traj_loc.reshape(-1)
+            adam_step_(u, self.m, self.v, self.grad[a:b], p, self.step_dev[0], self.lr, self.b1,
+                       self.b2, self.eps, self.bounds_loc, self.legacy, traj_base=tb,
+                       traj_stride=(b - a) if tb is not None else 0)
+        elif self.zero:
             rs = []
             for c in range(self.C):
                 md.engine_vjp_into(self.theta, self.h, self.grad, chunk=c)
@@ -317,7 +408,13 @@ class FusedAdamEngine:
         self.step_host += 1
         if self.history.mode != "full" and self.traj_loc is None:
             self.drain()
-            self.history.record(self.step_host - 1, self.theta[:self.P])
+            if self.owner:
+                st = self.history.stride
+                if self.step_host == self.history.nsteps or (st and self.step_host % st == 0):
+                    a, b = self.own_range
+                    self.history.record(self.step_host - 1, self._assemble(self.theta[a:b]))
+            else:
+                self.history.record(self.step_host - 1, self.theta[:self.P])
 
     def to_user(self, t: torch.Tensor) -> torch.Tensor:
         """Engine (internal) parameter order -> the model's parameter order (last dim)."""
@@ -330,6 +427,9 @@ class FusedAdamEngine:
         self.drain()
         if self.traj_loc is None:
             return self.to_user(self.history.result())
+        if self.owner:
+            rows = self.step_host + 1
+            return self.to_user(self._assemble(self.traj_loc[:rows].contiguous()))
         W = self.size
         nloc = self.traj_loc.shape[1]
         rows = self.step_host + 1
@@ -346,6 +446,9 @@ class FusedAdamEngine:
 
     def params(self) -> torch.Tensor:
         self.drain()
+        if self.owner:
+            a, b = self.own_range
+            return self.to_user(self._assemble(self.theta[a:b]))
         return self.to_user(self.theta[:self.P])
 
     def last_loss(self) -> float:
@@ -385,18 +488,28 @@ class _EngineObjective:
     def __init__(self, eng: FusedAdamEngine):
         self.e = eng
         self.comm = eng.comm
-        self.sharded = eng.zero
+        self.sharded = eng.zero or eng.owner
         self.device = eng.device
-        self.n_local = sum(eng.loc_len) if eng.zero else eng.P_pad
+        if eng.owner:
+            self.n_local = eng.own_range[1] - eng.own_range[0]
+        else:
+            self.n_local = sum(eng.loc_len) if eng.zero else eng.P_pad
 
     def x0(self) -> torch.Tensor:
         e = self.e
+        if e.owner:
+            a, b = e.own_range
+            return e.theta[a:b].clone()
         if not e.zero:
             return e.theta.clone()
         return torch.cat([e.theta[a:b] for a, b in e.own]).contiguous()
 
     def _load(self, x: torch.Tensor):
         e = self.e
+        if e.owner:
+            a, b = e.own_range
+            e.theta[a:b].copy_(x)
+            return
         if not e.zero:
             e.theta.copy_(x)
             return
@@ -412,7 +525,11 @@ class _EngineObjective:
         e, md = self.e, self.e.model
         self._load(x)
         e._forward_loss()
-        if e.zero:
+        if e.owner:
+            md.engine_vjp_into(e.theta, e.h, e.grad, chunk=e.rank)
+            a, b = e.own_range
+            g = e.grad[a:b]
+        elif e.zero:
             works = []
             for c in range(e.C):
                 md.engine_vjp_into(e.theta, e.h, e.grad, chunk=c)
@@ -435,4 +552,6 @@ class _EngineObjective:
         """The full parameter vector (model order) for the optimizer's vector x."""
         self._load(x)
         self.e.drain()
+        if self.e.owner:
+            return self.e.params().clone()
         return self.e.to_user(self.e.theta[:self.e.P]).clone()

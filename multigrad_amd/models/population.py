@@ -30,7 +30,7 @@ from ..ops.smf import (PopulationShard, SmfBins, logmse_loss, smf_edge_weights_i
 from ..parallel.comm import get_world_comm
 from .onepoint import OnePointModel
 
-__all__ = ["PopulationSMFModel", "make_population_data", "hash_uniform"]
+__all__ = ["PopulationSMFModel", "make_population_data", "hash_uniform", "owner_bounds"]
 
 _M1 = -7046029254386353131   # 0x9E3779B97F4A7C15 as int64
 _M2 = -4658895280553007687   # 0xBF58476D1CE4E5B9
@@ -56,11 +56,54 @@ def _rank_range(n: int, rank: int, size: int):
     return start, start + base + (1 if rank < rem else 0)
 
 
+_GEN_CHUNK = 1 << 24
+
+
+def _global_pop(idx: torch.Tensor, seed: int, npop: int) -> torch.Tensor:
+    return (_mix(idx, seed) & 0x7FFFFFFF) % npop
+
+
+def owner_bounds(num_halos: int, npop: int, seed: int, size: int, device) -> list:
+    """Population bounds ``Q[0..size]`` (even, so every owned parameter slice starts on a
+    16-byte boundary) that split the global catalog into ``size`` contiguous population
+    ranges of nearly equal halo counts -- ``np.array_split`` of the catalog sorted by
+    population, moved to the nearest population boundary so that no population straddles
+    two ranks.  Every rank derives the same bounds from the global counts (one pass over
+    the counter-based hash, no communication)."""
+    counts = torch.zeros(npop, dtype=torch.int64, device=device)
+    for a in range(0, int(num_halos), _GEN_CHUNK):
+        idx = torch.arange(a, min(int(num_halos), a + _GEN_CHUNK), dtype=torch.int64, device=device)
+        counts += torch.bincount(_global_pop(idx, seed, npop), minlength=npop)
+    cum = torch.cumsum(counts, 0).cpu().numpy()
+    bounds = [0]
+    for r in range(1, size):
+        target = r * int(num_halos) / size
+        q = int(np.searchsorted(cum, target, side="left")) + 1   # first pop after the split
+        q = min(max(q - (q & 1), bounds[-1]), npop)
+        bounds.append(q)
+    bounds.append(npop)
+    return bounds
+
+
 def make_population_data(num_params: int = 10_000_000, num_halos: int = 1 << 27, seed: int = 0,
                          comm=None, device=None, nbins: int = 10, chunks: int = 1,
                          truth_offset=(0.1, 0.1), tail: str = "absolute",
-                         layout: str = "lanes") -> dict:
+                         layout: str = "lanes", placement: str = "hashed") -> dict:
     """This rank's shard of the synthetic population-SMF data set.
+
+    The global catalog (halo i: population ``hash(i) mod J``, log mass from a second hash)
+    is the same for every placement and every number of ranks; ``placement`` only decides
+    which rank holds which halo:
+
+    ``"hashed"``: rank r holds the r-th contiguous block of halo indices (the reference's
+        ``np.array_split`` of an unsorted catalog).  Every rank touches every population,
+        so the gradient is dense on every rank and must be summed across ranks.
+    ``"owner"``: the catalog is split by population (:func:`owner_bounds`), as
+        ``np.array_split`` of a catalog sorted by population / host halo would (the
+        reference's diffdesi tree utilities sort by host, reference
+        multigrad/diffdesi_experimental/util.py:20-35).  Each rank's gradient is then
+        non-zero only on its own populations and the engine skips the gradient collective
+        (``data["owner_units"]``, see :class:`~multigrad_amd.engine.fused.FusedAdamEngine`).
 
     Returns a dict with the sorted device shard (``shard``), bins, volume, true
     parameters ``truth`` (interleaved, device) and a starting ``guess``; the target SMF is
@@ -68,13 +111,29 @@ def make_population_data(num_params: int = 10_000_000, num_halos: int = 1 << 27,
     """
     comm = get_world_comm() if comm is None else comm
     assert num_params % 2 == 0, "parameters come in (a, log_sigma) pairs"
+    if placement not in ("hashed", "owner"):
+        raise ValueError("placement must be 'hashed' or 'owner'")
     npop = num_params // 2
     if device is None:
         device = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() \
             else torch.device("cpu")
-    start, end = _rank_range(int(num_halos), comm.rank, comm.size)
-    idx = torch.arange(start, end, dtype=torch.int64, device=device)
-    pop = (_mix(idx, seed) & 0x7FFFFFFF) % npop
+    owner_units = None
+    if placement == "owner":
+        owner_units = owner_bounds(num_halos, npop, seed, comm.size, device)
+        lo, hi = owner_units[comm.rank], owner_units[comm.rank + 1]
+        parts = []
+        for a in range(0, int(num_halos), _GEN_CHUNK):
+            idx = torch.arange(a, min(int(num_halos), a + _GEN_CHUNK), dtype=torch.int64,
+                               device=device)
+            pp = _global_pop(idx, seed, npop)
+            parts.append(idx[(pp >= lo) & (pp < hi)])
+            del idx, pp
+        idx = torch.cat(parts) if parts else torch.zeros(0, dtype=torch.int64, device=device)
+        del parts
+    else:
+        start, end = _rank_range(int(num_halos), comm.rank, comm.size)
+        idx = torch.arange(start, end, dtype=torch.int64, device=device)
+    pop = _global_pop(idx, seed, npop)
     q = 0.9 * hash_uniform(idx, seed + 1)
     logm = (10.0 - torch.log10(1.0 - q)).to(torch.float32)          # log10(1e10/(1-q))
     del idx, q
@@ -93,7 +152,7 @@ def make_population_data(num_params: int = 10_000_000, num_halos: int = 1 << 27,
     volume = 10.0 * num_halos
     return dict(shard=shard, bins=SmfBins.make(edges, volume, tail), volume=volume, truth=truth,
                 guess=guess, npop=npop, num_halos=int(num_halos), target_sumstats=None,
-                loss_eps=1e-10)
+                loss_eps=1e-10, placement=placement, owner_units=owner_units)
 
 
 @dataclass(eq=False)
@@ -150,6 +209,18 @@ class PopulationSMFModel(OnePointModel):
 
     def engine_set_chunks(self, unit_bounds):
         self.shard.set_chunks(unit_bounds)
+
+    def engine_owner_units(self):
+        """Population (unit) bounds ``[W+1]`` of the owner placement, or None."""
+        return self.aux_data.get("owner_units")
+
+    def engine_support_units(self):
+        """``(lo, hi)``: the populations this rank's data touches lie in ``[lo, hi)``
+        (``(0, 0)`` for an empty shard)."""
+        nz = torch.nonzero(self.shard.counts > 0).reshape(-1)
+        if nz.numel() == 0:
+            return 0, 0
+        return int(nz[0]), int(nz[-1]) + 1
 
     def engine_param_perm(self):
         """Internal unit order of the engine vectors (lanes layout: populations in slot

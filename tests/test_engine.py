@@ -77,3 +77,74 @@ def test_engine_distributed_matches_single_rank(size, zero, chunks, bounded):
         np.testing.assert_allclose(traj, ref, rtol=3e-5, atol=3e-6)
         # every rank holds bitwise identical parameters (single owner per slice)
         np.testing.assert_array_equal(traj, res[0][0])
+
+
+def _owner_model(comm, placement):
+    data = make_population_data(num_params=NP, num_halos=NH, seed=11, comm=comm, device="cpu",
+                                placement=placement)
+    m = PopulationSMFModel(aux_data=data, comm=comm)
+    m.set_target_from_truth()
+    return m, data
+
+
+def _dist_owner(rank, size, bounded, history):
+    comm = mg.get_world_comm()
+    m, data = _owner_model(comm, "owner")
+    lo, hi = m.engine_support_units()
+    ub = data["owner_units"]
+    assert ub[rank] <= lo and hi <= ub[rank + 1]
+    bounds = [(-2.3, -1.6) if i % 2 == 0 else (None, -0.2) for i in range(NP)] if bounded else None
+    eng = FusedAdamEngine(m)
+    traj = eng.run_adam(data["guess"], nsteps=4, learning_rate=2e-3, param_bounds=bounds,
+                        history=history)
+    return traj.numpy(), eng.params().numpy(), float(eng.loss[0]), eng.owner, ub
+
+
+@pytest.mark.parametrize("size,bounded,history", [(2, False, "full"), (3, False, "full"),
+                                                  (2, True, "full"), (3, False, "last")])
+def test_engine_owner_placement_matches_single_rank(size, bounded, history):
+    """Population-owner placement: same global catalog, no gradient collective; the
+    trajectory equals the single-rank fit (the data set does not depend on placement)."""
+    res = run_distributed(_dist_owner, size, bounded, history)
+    bounds = [(-2.3, -1.6) if i % 2 == 0 else (None, -0.2) for i in range(NP)] if bounded else None
+    ref = _generic_traj(4, bounds).numpy()
+    if history == "last":
+        ref = ref[[0, -1]]
+    for traj, params, loss, owner, ub in res:
+        assert owner and len(ub) == size + 1
+        np.testing.assert_allclose(traj, ref, rtol=3e-5, atol=3e-6)
+        np.testing.assert_array_equal(traj[-1], params)
+        np.testing.assert_array_equal(traj, res[0][0])
+
+
+def _dist_owner_fallback(rank, size):
+    # hashed placement: every rank touches every population -> owner mode is refused
+    # collectively and the engine runs the dense ZeRO schedule
+    comm = mg.get_world_comm()
+    m, data = _owner_model(comm, "hashed")
+    m.aux_data["owner_units"] = [0, NP // 4, NP // 2][:size] + [NP // 2]
+    eng = FusedAdamEngine(m, chunks=2)
+    traj = eng.run_adam(data["guess"], nsteps=2, learning_rate=2e-3)
+    return eng.owner, eng.zero, traj.numpy()
+
+
+def test_engine_owner_mode_refused_for_dense_data():
+    res = run_distributed(_dist_owner_fallback, 2)
+    ref = _generic_traj(2).numpy()
+    for owner, zero, traj in res:
+        assert not owner and zero
+        np.testing.assert_allclose(traj, ref, rtol=3e-5, atol=3e-6)
+
+
+def test_owner_bounds_balanced():
+    from multigrad_amd.models.population import owner_bounds
+    J, N = 5000, 1 << 18
+    for W in (2, 3, 8):
+        ub = owner_bounds(N, J, 5, W, "cpu")
+        assert ub[0] == 0 and ub[-1] == J and all(u % 2 == 0 for u in ub[:-1])
+        assert all(a < b for a, b in zip(ub, ub[1:]))
+        idx = torch.arange(N)
+        from multigrad_amd.models.population import _global_pop
+        cnt = torch.bincount(_global_pop(idx, 5, J), minlength=J)
+        per = [int(cnt[a:b].sum()) for a, b in zip(ub, ub[1:])]
+        assert sum(per) == N and max(per) - min(per) <= 3 * 80, per

@@ -173,6 +173,24 @@ def test_engine_matches_generic_adam():
     assert float(loss) < float(loss0)
 
 
+def test_engine_owner_schedule_single_rank():
+    """The owner-mode schedule (own-chunk forward/VJP, owned-slice Adam with a strided
+    trajectory, assembly) on the HIP kernels, forced on one rank: equals the replicated
+    engine bitwise up to kernel-order effects."""
+    from multigrad_amd.engine.fused import FusedAdamEngine
+    from multigrad_amd.models.population import PopulationSMFModel, make_population_data
+    data = make_population_data(num_params=4000, num_halos=200_000, seed=3, device=DEV)
+    model = PopulationSMFModel(aux_data=data)
+    model.set_target_from_truth()
+    ref = FusedAdamEngine(model, graph=False).run_adam(data["guess"], nsteps=4, learning_rate=1e-3)
+    for graph in (False, True):
+        eng = FusedAdamEngine(model, graph=graph, owner=True)
+        t = eng.run_adam(data["guess"], nsteps=4, learning_rate=1e-3)
+        assert eng.owner
+        torch.testing.assert_close(t, ref, rtol=1e-6, atol=1e-7)
+        torch.testing.assert_close(eng.params(), t[-1], rtol=0, atol=0)
+
+
 def test_reference_pipeline_on_gpu():
     """Reference tests/test_mpi.py::test_simple_grad_descent_pipeline on the HIP path."""
     from multigrad_amd.models.smf import MySMFModel, ParamTuple, TARGET_SUMSTATS, make_test_data

@@ -85,9 +85,10 @@ def test_device_lbfgs_docs_model(size):
     assert all(r == res[0] for r in res)
 
 
-def _pop_lbfgs(rank, size, zero):
+def _pop_lbfgs(rank, size, zero, placement="hashed"):
     comm = mg.get_world_comm()
-    data = make_population_data(num_params=80, num_halos=3000, seed=3, comm=comm, device="cpu")
+    data = make_population_data(num_params=80, num_halos=3000, seed=3, comm=comm, device="cpu",
+                                placement=placement)
     m = PopulationSMFModel(aux_data=data, comm=comm)
     m.set_target_from_truth()
     res = m.run_bfgs(data["guess"], maxsteps=30, method="device", zero=zero, chunks=3)
@@ -98,6 +99,16 @@ def test_sharded_lbfgs_matches_single_rank():
     C.set_world_comm(None)
     x1, f1, n1 = _pop_lbfgs(0, 1, False)
     res = run_distributed(_pop_lbfgs, 2, True)
+    for x, f, nit in res:
+        np.testing.assert_allclose(x, x1, rtol=1e-3, atol=1e-4)
+        assert f == pytest.approx(f1, rel=1e-2, abs=1e-9)
+    np.testing.assert_array_equal(res[0][0], res[1][0])
+
+
+def test_sharded_lbfgs_owner_placement_matches_single_rank():
+    C.set_world_comm(None)
+    x1, f1, n1 = _pop_lbfgs(0, 1, False)
+    res = run_distributed(_pop_lbfgs, 3, True, "owner")
     for x, f, nit in res:
         np.testing.assert_allclose(x, x1, rtol=1e-3, atol=1e-4)
         assert f == pytest.approx(f1, rel=1e-2, abs=1e-9)
