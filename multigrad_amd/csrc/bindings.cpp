@@ -30,7 +30,9 @@ void smf_forward_lanes(torch::Tensor xi, torch::Tensor slot_pop, torch::Tensor g
                        std::vector<double> edges,
                        std::vector<double> scale, bool log_sigma, int64_t g0, int64_t g1,
                        torch::Tensor slab, int64_t nblocks, bool rel_tail,
-                       c10::optional<torch::Tensor> resid);
+                       c10::optional<torch::Tensor> resid,
+                       c10::optional<torch::Tensor> wave_order,
+                       c10::optional<torch::Tensor> wave_start);
 void smf_vjp_lanes(torch::Tensor slot_pop, torch::Tensor slot_part, torch::Tensor theta,
                    torch::Tensor h, torch::Tensor resid, int64_t s0, int64_t s1,
                    std::vector<double> scale, bool log_sigma, torch::Tensor grad,
@@ -40,7 +42,7 @@ void fused_adam(torch::Tensor u, torch::Tensor m, torch::Tensor v, torch::Tensor
                 c10::optional<torch::Tensor> p, c10::optional<torch::Tensor> lo,
                 c10::optional<torch::Tensor> hi, c10::optional<torch::Tensor> kind,
                 torch::Tensor step, double lr, double b1, double b2, double eps, bool legacy,
-                c10::optional<torch::Tensor> traj, int64_t traj_stride);
+                c10::optional<torch::Tensor> traj, int64_t traj_stride, int64_t host_step);
 // lbfgs.hip
 void multi_dot(torch::Tensor A, int64_t nrows, std::vector<torch::Tensor> B, int64_t n,
                torch::Tensor out, torch::Tensor workspace);
@@ -55,6 +57,8 @@ std::tuple<torch::Tensor, torch::Tensor> sort_by_population(torch::Tensor pop, i
 std::vector<torch::Tensor> build_lanes(torch::Tensor counts, std::vector<int64_t> breaks,
                                        int64_t window, int64_t lmax,
                                        c10::optional<torch::Tensor> order_counts);
+std::vector<torch::Tensor> lpt_waves(torch::Tensor group_len, torch::Tensor fwd_order,
+                                     int64_t g0, int64_t g1, int64_t nwaves, double overhead);
 }  // namespace mg
 
 PYBIND11_MODULE(_C, m) {
@@ -68,9 +72,19 @@ PYBIND11_MODULE(_C, m) {
   m.def("smf_vjp", &mg::smf_vjp);
   m.def("smf_fwd_lanes_max_blocks", &mg::smf_fwd_lanes_max_blocks);
   m.def("smf_lanes_pack", &mg::smf_lanes_pack);
-  m.def("smf_forward_lanes", &mg::smf_forward_lanes);
+  m.def("smf_forward_lanes", &mg::smf_forward_lanes, pybind11::arg("xi"), pybind11::arg("slot_pop"),
+        pybind11::arg("group_base"), pybind11::arg("group_len"), pybind11::arg("fwd_order"),
+        pybind11::arg("theta"), pybind11::arg("edges"), pybind11::arg("scale"),
+        pybind11::arg("log_sigma"), pybind11::arg("g0"), pybind11::arg("g1"), pybind11::arg("slab"),
+        pybind11::arg("nblocks"), pybind11::arg("rel_tail"), pybind11::arg("resid") = pybind11::none(),
+        pybind11::arg("wave_order") = pybind11::none(), pybind11::arg("wave_start") = pybind11::none());
+  m.def("lpt_waves", &mg::lpt_waves);
   m.def("smf_vjp_lanes", &mg::smf_vjp_lanes);
-  m.def("fused_adam", &mg::fused_adam);
+  m.def("fused_adam", &mg::fused_adam, pybind11::arg("u"), pybind11::arg("m"), pybind11::arg("v"),
+        pybind11::arg("g"), pybind11::arg("p"), pybind11::arg("lo"), pybind11::arg("hi"),
+        pybind11::arg("kind"), pybind11::arg("step"), pybind11::arg("lr"), pybind11::arg("b1"),
+        pybind11::arg("b2"), pybind11::arg("eps"), pybind11::arg("legacy"), pybind11::arg("traj"),
+        pybind11::arg("traj_stride"), pybind11::arg("host_step") = -1);
   m.def("multi_dot", &mg::multi_dot);
   m.def("multi_dot_workspace", &mg::multi_dot_workspace);
   m.def("lincomb", &mg::lincomb);

@@ -12,6 +12,7 @@
 #include <cstring>
 #include <cstdint>
 #include <tuple>
+#include <queue>
 #include <vector>
 
 namespace mg {
@@ -295,6 +296,51 @@ std::vector<torch::Tensor> build_lanes(torch::Tensor counts, std::vector<int64_t
   return {i32(slot_pop), i64(slot_src), i32(slot_len), i32(slot_part), i64(group_base),
           i32(group_len), i64(chunk_groups), i32(giant).reshape({-1, 3}), i64(chunk_giant),
           i32(fwd_order), i32(slot_pidx), i32(perm)};
+}
+
+
+// Static LPT (longest processing time first) assignment of the lanes groups [g0, g1) of
+// fwd_order to `nwaves` persistent wavefronts: groups in decreasing cost order go to
+// the currently least-loaded wave (binary heap).  A group costs its length in halo rows
+// plus `overhead` (parameter gather + residual stores, in halo-row units).  Round-robin
+// over the longest-first order is within a few % of this when every wave takes ~10+
+// groups (one GPU), but loses ~20% at 2-3 groups per wave (a population-owner shard on
+// each of 8 GPUs).  Returns (order [g1-g0] int32: group ids wave by wave,
+// wave_start [nwaves+1] int32).
+std::vector<torch::Tensor> lpt_waves(torch::Tensor group_len, torch::Tensor fwd_order,
+                                     int64_t g0, int64_t g1, int64_t nwaves, double overhead) {
+  TORCH_CHECK(group_len.device().is_cpu() && group_len.scalar_type() == at::kInt, "group_len: int32 CPU");
+  TORCH_CHECK(fwd_order.device().is_cpu() && fwd_order.scalar_type() == at::kInt, "fwd_order: int32 CPU");
+  TORCH_CHECK(nwaves >= 1 && g0 >= 0 && g0 <= g1 && g1 <= fwd_order.numel(), "bad LPT request");
+  auto gl = group_len.contiguous();
+  auto fo = fwd_order.contiguous();
+  const int32_t* len = gl.data_ptr<int32_t>();
+  const int32_t* ord = fo.data_ptr<int32_t>();
+  std::vector<int32_t> items(ord + g0, ord + g1);
+  std::stable_sort(items.begin(), items.end(),
+                   [&](int32_t a, int32_t b) { return len[a] > len[b]; });
+  using Load = std::pair<double, int64_t>;  // (load, wave): min-heap, ties -> lower wave
+  std::priority_queue<Load, std::vector<Load>, std::greater<Load>> heap;
+  for (int64_t w = 0; w < nwaves; ++w) heap.push({0.0, w});
+  std::vector<std::vector<int32_t>> lists(nwaves);
+  for (int32_t g : items) {
+    Load l = heap.top();
+    heap.pop();
+    lists[l.second].push_back(g);
+    l.first += (double)len[g] + overhead;
+    heap.push(l);
+  }
+  auto order = torch::empty({g1 - g0}, torch::kInt);
+  auto start = torch::empty({nwaves + 1}, torch::kInt);
+  int32_t* o = order.data_ptr<int32_t>();
+  int32_t* st = start.data_ptr<int32_t>();
+  int64_t pos = 0;
+  for (int64_t w = 0; w < nwaves; ++w) {
+    st[w] = (int32_t)pos;
+    for (int32_t g : lists[w]) o[pos++] = g;
+  }
+  st[nwaves] = (int32_t)pos;
+  return {order, start};
 }
 
 }  // namespace mg

@@ -611,7 +611,8 @@ __global__ __launch_bounds__(kThreads, MG_LANES_MINWAVES) void smf_fwd_lanes_ker
     const float* __restrict__ xi, const int32_t* __restrict__ slot_pop,
     const int64_t* __restrict__ group_base, const int32_t* __restrict__ group_len,
     const int32_t* __restrict__ fwd_order, const float2* __restrict__ theta, int64_t g0,
-    int64_t g1, SmfBins bins, float* __restrict__ slab, float* __restrict__ resid) {
+    int64_t g1, SmfBins bins, float* __restrict__ slab, float* __restrict__ resid,
+    const int32_t* __restrict__ wave_start) {
   float acc[NB + 1];
   int cnt[NB + 1];
 #pragma unroll
@@ -638,8 +639,13 @@ __global__ __launch_bounds__(kThreads, MG_LANES_MINWAVES) void smf_fwd_lanes_ker
   // memory counter never makes the next group wait for those stores), and the slot ->
   // population index is fetched one group further ahead, so the dependent theta gather
   // does not wait for a load issued in the same transition.
-  // positions k in [g0, g1) of the longest-first order; g = fwd_order[k] is the group
-  int64_t k = g0 + (int64_t)blockIdx.x * (kThreads / kWave) + wid;
+  // Work list: with wave_start (host LPT schedule, runtime.cpp:lpt_waves) wave w takes
+  // positions [wave_start[w], wave_start[w+1]) of its own list; otherwise positions
+  // k in [g0, g1) of the longest-first order, grid-strided.  g = fwd_order[k].
+  const int64_t w_id = (int64_t)blockIdx.x * (kThreads / kWave) + wid;
+  int64_t k = wave_start ? (int64_t)wave_start[w_id] : g0 + w_id;
+  const int64_t kstride = wave_start ? 1 : nwaves;
+  if (wave_start) g1 = wave_start[w_id + 1];
   int64_t g = 0;
   float2 th = make_float2(0.f, 0.f);
   const float* xp = xi;
@@ -653,7 +659,7 @@ __global__ __launch_bounds__(kThreads, MG_LANES_MINWAVES) void smf_fwd_lanes_ker
     len = group_len[g];
 #pragma unroll
     for (int u = 0; u < kLanesUnroll; ++u) xn[u] = lane_load(xp, u, len);
-    const int64_t ka = kk + nwaves;
+    const int64_t ka = kk + kstride;
     if (ka < g1) c_next = slot_pop[(int64_t)fwd_order[ka] * kWave + lane];
   };
   if (k < g1) load_group(k, slot_pop[(int64_t)fwd_order[k] * kWave + lane]);
@@ -705,7 +711,7 @@ __global__ __launch_bounds__(kThreads, MG_LANES_MINWAVES) void smf_fwd_lanes_ker
         lane_halo<NB, LOGSIG, REL, RESID>(xc[u], ninv, mua, bins, acc, cnt, G, W);
 #endif
     }
-    const int64_t kn = k + nwaves;
+    const int64_t kn = k + kstride;
     if (kn < g1) load_group(kn, c_next);
     if constexpr (RESID) {  // group-major [g][2 (NB+1)][64]: one contiguous block per group
       float* rg = resid + gc * (2 * (NB + 1) * kWave) + lane;
@@ -1083,7 +1089,9 @@ void smf_forward_lanes(torch::Tensor xi, torch::Tensor slot_pop, torch::Tensor g
                        std::vector<double> edges,
                        std::vector<double> scale, bool log_sigma, int64_t g0, int64_t g1,
                        torch::Tensor slab, int64_t nblocks, bool rel_tail,
-                       c10::optional<torch::Tensor> resid) {
+                       c10::optional<torch::Tensor> resid,
+                       c10::optional<torch::Tensor> wave_order,
+                       c10::optional<torch::Tensor> wave_start) {
   check_dev(xi, "xi", at::kFloat);
   check_dev(slot_pop, "slot_pop", at::kInt);
   check_dev(group_base, "group_base", at::kLong);
@@ -1106,6 +1114,19 @@ void smf_forward_lanes(torch::Tensor xi, torch::Tensor slot_pop, torch::Tensor g
                     resid->size(2) == kWave, "resid must be [ngroups, 2*(nbp+1), 64]");
     rp = resid->data_ptr<float>();
   }
+  const int32_t* order = fwd_order.data_ptr<int32_t>();
+  const int32_t* ws = nullptr;
+  if (wave_start.has_value() && wave_start->defined()) {
+    // per-wave LPT lists over the groups [g0, g1): every wave of the grid has an entry
+    TORCH_CHECK(wave_order.has_value() && wave_order->defined(), "wave_start needs wave_order");
+    check_dev(*wave_order, "wave_order", at::kInt);
+    check_dev(*wave_start, "wave_start", at::kInt);
+    TORCH_CHECK(wave_start->numel() == nblocks * (kThreads / kWave) + 1,
+                "wave_start must have one entry per wavefront of the grid (+1)");
+    TORCH_CHECK(wave_order->numel() == g1 - g0, "wave_order must list the chunk's groups");
+    order = wave_order->data_ptr<int32_t>();
+    ws = wave_start->data_ptr<int32_t>();
+  }
   const SmfBins b = make_bins(edges, scale, nbp);
   auto stream = at::hip::getCurrentHIPStream();
   const float2* tp = reinterpret_cast<const float2*>(theta.data_ptr<float>());
@@ -1114,8 +1135,8 @@ void smf_forward_lanes(torch::Tensor xi, torch::Tensor slot_pop, torch::Tensor g
       hipLaunchKernelGGL((smf_fwd_lanes_kernel<NB, decltype(LS)::value, decltype(RT)::value, decltype(RS)::value>),
                          dim3(nblocks), dim3(kThreads), 0, stream, xi.data_ptr<float>(),
                          slot_pop.data_ptr<int32_t>(), group_base.data_ptr<int64_t>(),
-                         group_len.data_ptr<int32_t>(), fwd_order.data_ptr<int32_t>(), tp, g0, g1, b,
-                         slab.data_ptr<float>(), rp);
+                         group_len.data_ptr<int32_t>(), order, tp, g0, g1, b,
+                         slab.data_ptr<float>(), rp, ws);
     }); }); });
   });
 }

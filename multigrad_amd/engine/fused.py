@@ -131,6 +131,7 @@ class FusedAdamEngine:
         g = _env_flag("MULTIGRAD_GRAPH", graph)
         self.use_graph = (self.size == 1) if g is None else bool(g)
         self.graph = None
+        self._capturing = False
         self.ready = False
 
     # ------------------------------------------------------------------ setup
@@ -340,7 +341,7 @@ class FusedAdamEngine:
             tb = None if self.traj_loc is None else self.traj_loc.reshape(-1)
             adam_step_(u, self.m, self.v, self.grad[a:b], p, self.step_dev[0], self.lr, self.b1,
                        self.b2, self.eps, self.bounds_loc, self.legacy, traj_base=tb,
-                       traj_stride=(b - a) if tb is not None else 0)
+                       traj_stride=(b - a) if tb is not None else 0, host_step=self._hstep())
         elif self.zero:
             rs = []
             for c in range(self.C):
@@ -359,7 +360,8 @@ class FusedAdamEngine:
                 adam_step_(u, self.m[o:o + n], self.v[o:o + n], self.g_loc[o:o + n], p,
                            self.step_dev[c], self.lr, self.b1, self.b2, self.eps,
                            self._bslice(c), self.legacy, traj_base=tb,
-                           traj_stride=self.traj_loc.shape[1] if tb is not None else 0)
+                           traj_stride=self.traj_loc.shape[1] if tb is not None else 0,
+                           host_step=self._hstep())
                 pa, L = self.pb[c], self.lengths[c]
                 agc = self.comm_ag if self.comm_ag is not None else self.comm
                 self._ag[c] = agc.all_gather_into_tensor(self.theta[pa:pa + L], self.theta[a:b],
@@ -379,20 +381,32 @@ class FusedAdamEngine:
                            self.theta[:P] if bnd is not None else None, self.step_dev[0],
                            self.lr, self.b1, self.b2, self.eps,
                            None if bnd is None else Bounds(bnd.lo[:P], bnd.hi[:P], bnd.kind[:P]),
-                           self.legacy, traj_base=hb, traj_stride=stride)
+                           self.legacy, traj_base=hb, traj_stride=stride, host_step=self._hstep())
             else:
                 adam_step_(self.u, self.m, self.v, self.grad,
                            self.theta if bnd is not None else None, self.step_dev[0],
                            self.lr, self.b1, self.b2, self.eps, bnd, self.legacy,
-                           traj_base=hb, traj_stride=stride)
+                           traj_base=hb, traj_stride=stride, host_step=self._hstep())
+
+    def _hstep(self):
+        """The 0-based step for eager launches; None inside a graph capture (the Adam
+        kernel then keeps the step in device memory so the replay self-advances)."""
+        return None if self._capturing else self.step_host
 
     def _capture(self):
+        prep = getattr(self.model, "engine_prepare", None)
+        if prep is not None:
+            prep([self.rank] if self.owner else list(range(self.C)))
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         torch.cuda.current_stream().wait_stream(s)
         self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph):
-            self._enqueue_step()
+        self._capturing = True
+        try:
+            with torch.cuda.graph(self.graph):
+                self._enqueue_step()
+        finally:
+            self._capturing = False
 
     def step(self):
         """Enqueue one optimizer step (asynchronous on GPU)."""

@@ -24,7 +24,7 @@ from typing import Optional
 import numpy as np
 import torch
 
-from ..ops.smf import (PopulationShard, SmfBins, logmse_loss, smf_edge_weights_into,
+from ..ops.smf import (PopulationShard, SmfBins, logmse_loss, prepare_forward, smf_edge_weights_into,
                        smf_forward_into, smf_forward_slab, smf_slab_reduce, smf_sumstats,
                        smf_vjp_into)
 from ..parallel.comm import get_world_comm
@@ -245,6 +245,12 @@ class PopulationSMFModel(OnePointModel):
         # so the forward stores the VJP residuals (lanes layout)
         return smf_forward_slab(theta, self.shard, self.bins, True, slab, chunk, resid=True,
                                 order=self._engine_order())
+
+    def engine_prepare(self, chunks):
+        """Host-side schedule construction for the given chunks (called by the engine
+        before it captures a step into a HIP graph)."""
+        for c in chunks:
+            prepare_forward(self.shard, self.bins, True, c)
 
     def engine_reduce(self, slab, nrows, S):
         return smf_slab_reduce(slab, nrows, self.bins, S)

@@ -14,13 +14,15 @@ def fused_adam_(u: torch.Tensor, m: torch.Tensor, v: torch.Tensor, g: torch.Tens
                 p: Optional[torch.Tensor], step: torch.Tensor, lr: float, b1: float, b2: float,
                 eps: float, bounds=None, legacy: bool = False,
                 traj_row: Optional[torch.Tensor] = None, traj_base: Optional[torch.Tensor] = None,
-                traj_stride: int = 0) -> None:
+                traj_stride: int = 0, host_step: Optional[int] = None) -> None:
     """One in-place Adam step on device.
 
     ``step`` is a ``[2]`` int32 device tensor ``[step, ticket]``; the kernel reads the
     0-based step for bias correction and advances it.  Either ``traj_row`` (eager: the
     row for this step) or ``traj_base``/``traj_stride`` (graph-replayable: row
-    ``step+1`` is computed on the device) may be given.
+    ``step+1`` is computed on the device) may be given.  ``host_step`` (eager callers
+    only, never inside a graph capture) supplies the 0-based step directly; the device
+    counter is then neither read nor advanced.
     """
     if traj_row is not None:
         # express the eager row through the device-step formula: base = row - (step+1)*stride
@@ -30,10 +32,11 @@ def fused_adam_(u: torch.Tensor, m: torch.Tensor, v: torch.Tensor, g: torch.Tens
     if bounds is not None:
         ext().fused_adam(u, m, v, g, p, bounds.lo, bounds.hi, bounds.kind, step, float(lr),
                          float(b1), float(b2), float(eps), bool(legacy), traj_base,
-                         int(traj_stride))
+                         int(traj_stride), -1 if host_step is None else int(host_step))
     else:
         ext().fused_adam(u, m, v, g, None, None, None, None, step, float(lr), float(b1),
-                         float(b2), float(eps), False, traj_base, int(traj_stride))
+                         float(b2), float(eps), False, traj_base, int(traj_stride),
+                         -1 if host_step is None else int(host_step))
 
 
 def adam_reference_(u, m, v, g, step: int, lr, b1, b2, eps):
@@ -46,14 +49,16 @@ def adam_reference_(u, m, v, g, step: int, lr, b1, b2, eps):
 
 
 def adam_step_(u, m, v, g, p, step: torch.Tensor, lr, b1, b2, eps, bounds=None,
-               legacy: bool = False, traj_base=None, traj_stride: int = 0) -> None:
+               legacy: bool = False, traj_base=None, traj_stride: int = 0,
+               host_step: Optional[int] = None) -> None:
     """Device-agnostic in-place Adam step: the fused HIP kernel on GPU tensors, the same
-    arithmetic in PyTorch on CPU tensors (``step`` is then a CPU ``[2]`` int tensor)."""
+    arithmetic in PyTorch on CPU tensors (``step`` is then a CPU ``[2]`` int tensor).
+    ``host_step``: see :func:`fused_adam_` (the CPU path then leaves ``step`` alone)."""
     if u.device.type == "cuda":
         fused_adam_(u, m, v, g, p, step, lr, b1, b2, eps, bounds, legacy,
-                    traj_base=traj_base, traj_stride=traj_stride)
+                    traj_base=traj_base, traj_stride=traj_stride, host_step=host_step)
         return
-    i = int(step[0])
+    i = int(step[0]) if host_step is None else int(host_step)
     gg = g
     if bounds is not None:
         at = p if legacy else u
@@ -69,4 +74,5 @@ def adam_step_(u, m, v, g, p, step: torch.Tensor, lr, b1, b2, eps, bounds=None,
     if traj_base is not None:
         n = u.numel()
         traj_base[(i + 1) * traj_stride:(i + 1) * traj_stride + n].copy_(newp)
-    step[0] = i + 1
+    if host_step is None:
+        step[0] = i + 1

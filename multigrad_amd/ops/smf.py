@@ -7,6 +7,7 @@ below, which is also the numerics oracle for the kernel tests.
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass, field
 from typing import List, Optional, Sequence
 
@@ -23,6 +24,7 @@ TILE_POPS = 2048
 FWD_BLOCKS_MAX = 2048  # 8 workgroups per CU on 256 CUs, grid-stride beyond
 LANE_WINDOW = 4096     # lanes layout: populations sorted by size within windows of this many
 LANE_LMAX = 4096       # lanes layout: populations with more halos are split into parts
+LPT_OVERHEAD = float(os.environ.get("MULTIGRAD_LPT_OVERHEAD", "3"))  # per-group cost, halo rows
 
 
 @dataclass(frozen=True)
@@ -225,6 +227,8 @@ class PopulationShard:
         self.group_base = group_base.to(dev)
         self.group_len = group_len.to(dev)
         self.fwd_order = fwd_order.to(dev)
+        self._group_len_cpu, self._fwd_order_cpu = group_len.cpu(), fwd_order.cpu()
+        self._wave_cache = {}
         self.giant = giant.to(dev).contiguous()
         # internal parameter order (see build_lanes): perm[i] = population of unit i
         self.slot_pidx = slot_pidx.to(dev)
@@ -248,6 +252,22 @@ class PopulationShard:
             self.xi = None
         self.resid = None
         self.resid_epoch += 1
+
+    def wave_schedule(self, chunk: Optional[int], nblocks: int):
+        """Per-wavefront LPT work lists for the lanes forward over ``chunk`` with a grid
+        of ``nblocks`` workgroups (runtime.cpp:lpt_waves), or ``(None, None)`` when
+        disabled (``MULTIGRAD_LPT=0``: grid-stride over the longest-first order)."""
+        if os.environ.get("MULTIGRAD_LPT", "1") == "0":
+            return None, None
+        key = (chunk, int(nblocks))
+        if key not in self._wave_cache:
+            if self.device.type == "cuda" and torch.cuda.is_current_stream_capturing():
+                return None, None  # no host->device copies inside a graph capture
+            g0, g1 = self.group_range(chunk)
+            order, start = ext().lpt_waves(self._group_len_cpu, self._fwd_order_cpu, g0, g1,
+                                           int(nblocks) * (256 // 64), LPT_OVERHEAD)
+            self._wave_cache[key] = (order.to(self.device), start.to(self.device))
+        return self._wave_cache[key]
 
     def resid_buffer(self, nbp: int) -> torch.Tensor:
         """Residual storage of the lanes forward, group-major [ngroups, 2 (nbp+1), 64]."""
@@ -354,16 +374,28 @@ def smf_forward_slab(theta: torch.Tensor, shard: PopulationShard, bins: SmfBins,
     if shard.layout == "lanes":
         g0, g1 = shard.group_range(chunk)
         rbuf = shard.resid_buffer(bins.nbp) if resid else None
+        w_order, w_start = shard.wave_schedule(chunk, nblk)
         ext().smf_forward_lanes(shard.xi, shard.slot_index(order), shard.group_base,
                                 shard.group_len, shard.fwd_order, theta, list(bins.edges),
                                 list(bins.scale), bool(log_sigma), g0, g1, slab, nblk,
-                                bins.rel_tail, rbuf)
+                                bins.rel_tail, rbuf, w_order, w_start)
         if resid:
             shard.resid_epoch += 1
         return nblk
     ext().smf_forward(shard.x, shard.pop, theta, list(bins.edges), list(bins.scale),
                       bool(log_sigma), h0, h1, slab, nblk, bins.rel_tail)
     return nblk
+
+
+def prepare_forward(shard: "PopulationShard", bins: SmfBins, log_sigma: bool = True,
+                    chunk: Optional[int] = None) -> None:
+    """Build (outside any graph capture) the host-side schedules the forward over
+    ``chunk`` will use, e.g. the lanes layout's per-wave LPT lists."""
+    if shard.device.type != "cuda" or shard.layout != "lanes":
+        return
+    h0, h1 = shard.halo_range(chunk)
+    nblk = shard.fwd_blocks(max(h1 - h0, 1), bins.nb, log_sigma, bins.rel_tail, chunk)
+    shard.wave_schedule(chunk, nblk)
 
 
 def smf_slab_reduce(slab: torch.Tensor, nrows: int, bins: SmfBins, out: torch.Tensor) -> torch.Tensor:
