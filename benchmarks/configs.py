@@ -20,6 +20,9 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 os.environ.setdefault("MULTIGRAD_PROGRESS", "0")
 
 
+PLACEMENT = "hashed"
+
+
 def _sync():
     import torch
     if torch.cuda.is_available():
@@ -44,7 +47,8 @@ def adam(comm, steps, params, halos, history):
     import torch
     from multigrad_amd.models.population import PopulationSMFModel, make_population_data
     dev = torch.device("cuda", torch.cuda.current_device())
-    data = make_population_data(params, halos, seed=1234, comm=comm, device=dev)
+    data = make_population_data(params, halos, seed=1234, comm=comm, device=dev,
+                                placement=PLACEMENT)
     m = PopulationSMFModel(aux_data=data, comm=comm)
     m.set_target_from_truth()
     eng = m.fused_engine()
@@ -67,7 +71,8 @@ def lbfgs(comm, iters, params, halos):
     from multigrad_amd.models.population import PopulationSMFModel, make_population_data
     from multigrad_amd.optim.lbfgs import lbfgs_minimize
     dev = torch.device("cuda", torch.cuda.current_device())
-    data = make_population_data(params, halos, seed=1234, comm=comm, device=dev)
+    data = make_population_data(params, halos, seed=1234, comm=comm, device=dev,
+                                placement=PLACEMENT)
     m = PopulationSMFModel(aux_data=data, comm=comm)
     m.set_target_from_truth()
     obj = m.fused_engine().lbfgs_objective(data["guess"])
@@ -86,7 +91,12 @@ def main(argv=None):
     ap.add_argument("--which", nargs="+", default=["toy", "adam1e6", "lbfgs"])
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--halos", type=int, default=1 << 27)
+    ap.add_argument("--placement", default="hashed", choices=["hashed", "owner"],
+                    help="multi-rank data placement: 'hashed' (dense gradient: the data-parallel "
+                         "RCCL configs 3-5) or 'owner' (population-owner shards)")
     args = ap.parse_args(argv)
+    global PLACEMENT
+    PLACEMENT = args.placement
     import torch
     import multigrad_amd as mg
     comm = mg.init_distributed() if int(os.environ.get("WORLD_SIZE", "1")) > 1 else mg.get_world_comm()

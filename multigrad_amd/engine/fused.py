@@ -475,17 +475,114 @@ class FusedAdamEngine:
         self.setup(guess, nsteps=1, history="last")
         return _EngineObjective(self)
 
+    # ------------------------------------------------------------------ checkpoints
+    @property
+    def sharded(self) -> bool:
+        return self.size > 1 and (self.zero or self.owner)
+
+    def _local_theta(self) -> torch.Tensor:
+        if self.owner:
+            a, b = self.own_range
+            return self.theta[a:b]
+        if self.zero:
+            return torch.cat([self.theta[a:b] for a, b in self.own])
+        return self.theta
+
+    def state_dict(self) -> dict:
+        """This rank's optimizer state after ``step_host`` steps: owned slices under ZeRO
+        and owner mode (one file per rank), everything otherwise."""
+        self.drain()
+        mode = "owner" if self.owner else "zero" if self.zero else "replicated"
+        u = self.u_loc if self.sharded else (self.u if self.bounds is not None else None)
+        st = {"mode": mode, "size": self.size, "rank": self.rank, "P": self.P,
+              "pb": list(self.pb), "step": self.step_host, "lr": self.lr,
+              "theta": self._local_theta().detach().cpu().clone(),
+              "m": self.m.detach().cpu().clone(), "v": self.v.detach().cpu().clone(),
+              "u": None if u is None else u.detach().cpu().clone()}
+        rows = self.step_host + 1
+        if self.traj_loc is not None:
+            st["traj"] = self.traj_loc[:rows].detach().cpu().clone()
+        elif self.history.mode == "full":
+            st["traj"] = self.history.buf[:rows].detach().cpu().clone()
+        else:
+            st["history_rows"] = [r.detach().cpu().clone() for r in self.history.rows]
+        return st
+
+    def load_state_dict(self, st: dict) -> int:
+        """Restore a :meth:`state_dict` into a :meth:`setup` engine of the same shape;
+        returns the step to continue from."""
+        mode = "owner" if self.owner else "zero" if self.zero else "replicated"
+        if st["mode"] != mode or st["size"] != self.size or st["P"] != self.P or \
+                list(st["pb"]) != list(self.pb):
+            raise ValueError(f"checkpoint ({st['mode']}, {st['size']} ranks) does not match "
+                             f"this engine ({mode}, {self.size} ranks)")
+        dev = self.device
+        step = int(st["step"])
+        self.m.copy_(st["m"].to(dev))
+        self.v.copy_(st["v"].to(dev))
+        th = st["theta"].to(dev)
+        if self.owner:
+            a, b = self.own_range
+            self.theta[a:b].copy_(th)
+        elif self.zero:
+            for c in range(self.C):
+                a, b = self.own[c]
+                o, n = self.loc_off[c], self.loc_len[c]
+                self.theta[a:b].copy_(th[o:o + n])
+                pa, L = self.pb[c], self.lengths[c]
+                agc = self.comm_ag if self.comm_ag is not None else self.comm
+                self._ag[c] = agc.all_gather_into_tensor(self.theta[pa:pa + L], self.theta[a:b],
+                                                         async_op=True)
+            self.drain()
+        else:
+            self.theta.copy_(th)
+        if st.get("u") is not None:
+            (self.u_loc if self.sharded else self.u).copy_(st["u"].to(dev))
+        elif not self.sharded and self.bounds is None:
+            self.u = self.theta
+        if "traj" in st:
+            tr = st["traj"].to(dev)
+            dst = self.traj_loc if self.traj_loc is not None else self.history.buf
+            dst[:tr.shape[0]].copy_(tr)
+        elif "history_rows" in st:
+            self.history.rows = [r.to(dev) for r in st["history_rows"]]
+        self.step_host = step
+        self.step_dev[:, 0] = step
+        self.step_dev[:, 1] = 0
+        return step
+
+    def save_checkpoint(self, path: str) -> None:
+        from ..utils import checkpoint as ckpt
+        ckpt.save_optimizer_state(path, self.state_dict(), comm=self.comm if self.size > 1 else None,
+                                  sharded=self.sharded)
+
+    def load_checkpoint(self, path: str) -> int:
+        from ..utils import checkpoint as ckpt
+        return self.load_state_dict(ckpt.load_optimizer_state(path, rank=self.rank,
+                                                              sharded=self.sharded))
+
     # ------------------------------------------------------------------ driver
     def run_adam(self, guess, nsteps: int = 100, param_bounds=None, learning_rate: float = 0.01,
                  b1: float = 0.9, b2: float = 0.999, eps: float = 1e-8, history="full",
-                 legacy_bounds_jacobian: bool = False, callback=None, **unused):
-        """Adam with the reference's return contract: trajectory ``(nsteps+1, P)``."""
+                 legacy_bounds_jacobian: bool = False, callback=None,
+                 checkpoint_path: Optional[str] = None, checkpoint_every: int = 0,
+                 resume_from: Optional[str] = None, **unused):
+        """Adam with the reference's return contract: trajectory ``(nsteps+1, P)``.
+
+        ``checkpoint_path``/``checkpoint_every`` write a resumable state every k steps
+        (owner-/ZeRO-sharded runs write one file per rank, ``<path>.rank<r>``);
+        ``resume_from`` continues such a run (same number of ranks and placement)."""
+        if unused:
+            raise TypeError(f"unsupported run_adam options for the fused engine: {sorted(unused)}")
         self.setup(guess, nsteps, param_bounds, learning_rate, b1, b2, eps, history,
                    legacy_bounds_jacobian)
-        for i in range(int(nsteps)):
+        start = self.load_checkpoint(resume_from) if resume_from is not None else 0
+        for i in range(start, int(nsteps)):
             self.step()
             if callback is not None:
                 callback(i, self.loss, self)
+            if checkpoint_path and checkpoint_every and (i + 1) % checkpoint_every == 0:
+                self.save_checkpoint(checkpoint_path)
         return self.trajectory()
 
 

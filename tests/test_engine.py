@@ -148,3 +148,47 @@ def test_owner_bounds_balanced():
         cnt = torch.bincount(_global_pop(idx, 5, J), minlength=J)
         per = [int(cnt[a:b].sum()) for a, b in zip(ub, ub[1:])]
         assert sum(per) == N and max(per) - min(per) <= 3 * 80, per
+
+
+def _resume_run(rank, size, placement, tmp, history, bounded):
+    comm = mg.get_world_comm() if size > 1 else None
+    if comm is None:
+        C.set_world_comm(None)
+    m, data = _owner_model(comm, placement)
+    bounds = [(-2.3, -1.6) if i % 2 == 0 else (None, -0.2) for i in range(NP)] if bounded else None
+    kw = dict(learning_rate=2e-3, param_bounds=bounds, history=history)
+    full = FusedAdamEngine(m, chunks=2).run_adam(data["guess"], nsteps=6, **kw)
+    ck = f"{tmp}/eng.ckpt"
+    e1 = FusedAdamEngine(m, chunks=2)
+    # a run of nsteps=6 interrupted after 4 steps, with its checkpoint from step 3
+    e1.setup(data["guess"], 6, bounds, 2e-3, history=history)
+    for i in range(4):
+        e1.step()
+        if i + 1 == 3:
+            e1.save_checkpoint(ck)
+    e2 = FusedAdamEngine(m, chunks=2)
+    resumed = e2.run_adam(data["guess"], nsteps=6, resume_from=ck, **kw)
+    mode = "owner" if e2.owner else "zero" if e2.zero else "replicated"
+    return full.numpy(), resumed.numpy(), mode
+
+
+@pytest.mark.parametrize("size,placement,history,bounded",
+                         [(1, "hashed", "full", False), (1, "hashed", "last", True),
+                          (2, "hashed", "full", True), (2, "owner", "full", False),
+                          (3, "owner", "last", True)])
+def test_engine_checkpoint_resume(tmp_path, size, placement, history, bounded):
+    if size == 1:
+        res = [_resume_run(0, 1, placement, str(tmp_path), history, bounded)]
+    else:
+        res = run_distributed(_resume_run, size, placement, str(tmp_path), history, bounded)
+    for full, resumed, mode in res:
+        assert mode == {("hashed", 1): "replicated", ("hashed", 2): "zero"}.get(
+            (placement, size), "owner")
+        np.testing.assert_array_equal(resumed, full)
+
+
+def test_engine_rejects_unknown_options():
+    C.set_world_comm(None)
+    m, data = _model()
+    with pytest.raises(TypeError):
+        FusedAdamEngine(m).run_adam(data["guess"], nsteps=1, not_an_option=3)
