@@ -7,13 +7,18 @@ each GPU from a hash of the global halo index (strong scaling: the global data s
 fixed, each of N ranks owns 1/N of it), random-init truth parameters.
 
 Every timed step does the full work of the reference's Adam step
-(multigrad/adam.py:59-66 + multigrad/multigrad.py:508-538): forward over all local
-halos, all-reduce of the sumstats, loss + cotangent, VJP over all local halos, the
-cross-rank sum of the dense 1e7-float gradient, the Adam update of all 1e7 parameters,
-and the trajectory write of the new parameters.  On one GPU the step is a replayed HIP
-graph; on N GPUs the gradient sum is a chunked RCCL reduce-scatter (overlapped with the
-VJP), Adam runs on each rank's 1/N slice, and the parameters come back with an in-place
-all-gather (ZeRO-1) -- the same bytes as one all-reduce.
+(multigrad/adam.py:59-66 + multigrad/multigrad.py:508-538): forward over all halos,
+all-reduce of the sumstats, loss + cotangent, VJP over all halos, the cross-rank
+gradient sum, the Adam update of all 1e7 parameters, and the trajectory write of the new
+parameters.  On one GPU the step is a replayed HIP graph.  On N GPUs (one process per
+GPU, RCCL) the default ``--placement owner`` splits the global catalog by population:
+each rank's gradient is then complete on the populations it owns and zero elsewhere, so
+the per-step collective is the 10-float sumstat all-reduce and every rank updates (and
+records the trajectory of) only its own parameters.  ``--placement hashed`` splits the
+catalog by halo index instead: every rank's gradient is dense and the engine runs a
+chunked RCCL reduce-scatter (overlapped with the VJP), Adam on each rank's 1/N slice and
+an in-place all-gather (ZeRO-1) -- the same bytes as one all-reduce.  Both placements
+hold the same global data set and give the same trajectory (tests/test_engine.py).
 
 Usage: ``python bench.py [--gpus N] [--steps K] [--warmup W]``; for N>1 launch with
 ``python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py``.
@@ -59,7 +64,14 @@ def main(argv=None):
         comm = mg.get_world_comm()
     if torch.cuda.is_available():
         torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")) % torch.cuda.device_count())
-    dev = torch.device("cuda", torch.cuda.current_device())
+    # CPU fallback (PyTorch reference math) only so the JSON contract is testable without a
+    # GPU; every measured number comes from the HIP path
+    dev = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() \
+        else torch.device("cpu")
+
+    def sync():
+        if dev.type == "cuda":
+            torch.cuda.synchronize()
 
     t_setup = time.perf_counter()
     data = make_population_data(args.params, args.halos, seed=1234, comm=comm, device=dev,
@@ -67,23 +79,26 @@ def main(argv=None):
     model = PopulationSMFModel(aux_data=data, comm=comm)
     model.set_target_from_truth()
     history = args.history if args.history in ("full", "last") else int(args.history)
-    engine = model.fused_engine(graph=None if not args.no_graph else False)
+    engine = model.fused_engine(graph=False if (args.no_graph or args.profile_phases) else None)
+    if args.profile_phases:  # HIP-event timing per phase (eager launches; stderr summary)
+        from multigrad_amd.utils.profiling import PhaseTimer
+        engine.timer = PhaseTimer(True)
     engine.setup(data["guess"], nsteps=args.warmup + args.steps, learning_rate=args.lr,
                  history=history)
-    torch.cuda.synchronize()
+    sync()
     setup_s = time.perf_counter() - t_setup
 
     for _ in range(args.warmup):
         engine.step()
     loss0 = engine.last_loss()
-    torch.cuda.synchronize()
+    sync()
     comm.barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         engine.step()
     engine.drain()  # last all-gathers joined into the compute stream
-    torch.cuda.synchronize()
+    sync()
     comm.barrier()
     elapsed = time.perf_counter() - t0
     loss1 = engine.last_loss()
@@ -130,6 +145,8 @@ def main(argv=None):
         "loss_last": loss1,
         "setup_s": round(setup_s, 2),
     }
+    if args.profile_phases:
+        rec["phases_ms"] = {k: round(v, 4) for k, v in engine.timer.summary().items()}
     if comm.rank == 0:
         print(json.dumps(rec), flush=True)
     if comm.size > 1:

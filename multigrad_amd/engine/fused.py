@@ -56,9 +56,12 @@ from typing import List, Optional
 
 import torch
 
+import contextlib
+
 from ..optim.adam import History
 from ..optim.transforms import Bounds, KIND_NONE
 from ..ops.adam import adam_step_
+from ..utils.profiling import PhaseTimer
 
 __all__ = ["FusedAdamEngine", "plan_chunks"]
 
@@ -133,6 +136,9 @@ class FusedAdamEngine:
         self.graph = None
         self._capturing = False
         self.ready = False
+        # per-phase HIP-event timing of eager steps (MULTIGRAD_PROFILE=1 or bench.py
+        # --profile-phases); never active inside a graph capture
+        self.timer = PhaseTimer()
 
     # ------------------------------------------------------------------ setup
     def setup(self, guess, nsteps: int, param_bounds=None, learning_rate: float = 0.01,
@@ -296,6 +302,11 @@ class FusedAdamEngine:
             out[..., a:b] = gathered[r][..., :b - a]
         return out
 
+    def _ph(self, name: str):
+        if self._capturing or not self.timer.enabled:
+            return contextlib.nullcontext()
+        return self.timer.phase(name)
+
     def _bslice(self, c):
         if self.bounds_loc is None:
             return None
@@ -319,14 +330,17 @@ class FusedAdamEngine:
     def _forward_loss(self):
         md = self.model
         row = 0
-        for c in ([self.rank] if self.owner else range(self.C)):
-            self._drain(c)
-            n = md.engine_forward_chunk(self.theta, self.slab[row * self.nS:], c)
-            row += n
-        md.engine_reduce(self.slab, row, self.S)
+        with self._ph("forward"):
+            for c in ([self.rank] if self.owner else range(self.C)):
+                self._drain(c)
+                n = md.engine_forward_chunk(self.theta, self.slab[row * self.nS:], c)
+                row += n
+            md.engine_reduce(self.slab, row, self.S)
         if self.size > 1:
-            self.comm.all_reduce(self.S)
-        md.engine_loss_into(self.S, self.loss, self.h)
+            with self._ph("sumstat_allreduce"):
+                self.comm.all_reduce(self.S)
+        with self._ph("loss"):
+            md.engine_loss_into(self.S, self.loss, self.h)
 
     def _enqueue_step(self):
         md = self.model
@@ -334,59 +348,72 @@ class FusedAdamEngine:
         hb = self.history.buf.reshape(-1) if self.history.mode == "full" else None
         if self.owner:
             c = self.rank
-            md.engine_vjp_into(self.theta, self.h, self.grad, chunk=c)
+            with self._ph("vjp"):
+                md.engine_vjp_into(self.theta, self.h, self.grad, chunk=c)
             a, b = self.own_range
             u = self.u_loc if self.u_loc is not None else self.theta[a:b]
             p = self.theta[a:b] if self.u_loc is not None else None
             tb = None if self.traj_loc is None else self.traj_loc.reshape(-1)
-            adam_step_(u, self.m, self.v, self.grad[a:b], p, self.step_dev[0], self.lr, self.b1,
-                       self.b2, self.eps, self.bounds_loc, self.legacy, traj_base=tb,
-                       traj_stride=(b - a) if tb is not None else 0, host_step=self._hstep())
+            with self._ph("adam"):
+                adam_step_(u, self.m, self.v, self.grad[a:b], p, self.step_dev[0], self.lr,
+                           self.b1, self.b2, self.eps, self.bounds_loc, self.legacy,
+                           traj_base=tb, traj_stride=(b - a) if tb is not None else 0,
+                           host_step=self._hstep())
         elif self.zero:
             rs = []
             for c in range(self.C):
-                md.engine_vjp_into(self.theta, self.h, self.grad, chunk=c)
+                with self._ph("vjp"):
+                    md.engine_vjp_into(self.theta, self.h, self.grad, chunk=c)
                 a, L = self.pb[c], self.lengths[c]
                 o, n = self.loc_off[c], self.loc_len[c]
                 rs.append(self.comm.reduce_scatter_tensor(self.g_loc[o:o + n], self.grad[a:a + L],
                                                           async_op=True))
             for c in range(self.C):
-                rs[c].wait()
+                with self._ph("grad_reduce_scatter_wait"):
+                    rs[c].wait()
                 a, b = self.own[c]
                 o, n = self.loc_off[c], self.loc_len[c]
                 u = self.u_loc[o:o + n] if self.u_loc is not None else self.theta[a:b]
                 p = self.theta[a:b] if self.u_loc is not None else None
                 tb = None if self.traj_loc is None else self.traj_loc.reshape(-1)[o:]
-                adam_step_(u, self.m[o:o + n], self.v[o:o + n], self.g_loc[o:o + n], p,
-                           self.step_dev[c], self.lr, self.b1, self.b2, self.eps,
-                           self._bslice(c), self.legacy, traj_base=tb,
-                           traj_stride=self.traj_loc.shape[1] if tb is not None else 0,
-                           host_step=self._hstep())
+                with self._ph("adam"):
+                    adam_step_(u, self.m[o:o + n], self.v[o:o + n], self.g_loc[o:o + n], p,
+                               self.step_dev[c], self.lr, self.b1, self.b2, self.eps,
+                               self._bslice(c), self.legacy, traj_base=tb,
+                               traj_stride=self.traj_loc.shape[1] if tb is not None else 0,
+                               host_step=self._hstep())
                 pa, L = self.pb[c], self.lengths[c]
                 agc = self.comm_ag if self.comm_ag is not None else self.comm
                 self._ag[c] = agc.all_gather_into_tensor(self.theta[pa:pa + L], self.theta[a:b],
                                                          async_op=True)
         else:
-            for c in range(self.C):
-                md.engine_vjp_into(self.theta, self.h, self.grad, chunk=c if self.C > 1 else None)
+            with self._ph("vjp"):
+                for c in range(self.C):
+                    md.engine_vjp_into(self.theta, self.h, self.grad,
+                                       chunk=c if self.C > 1 else None)
             if self.size > 1:
-                self.comm.all_reduce(self.grad)
-            stride = self.P if hb is not None else 0
-            bnd = self.bounds
-            if hb is not None and self.P_pad != self.P:
-                # trajectory rows are P long: update the real parameters and the padding
-                # separately so the kernel writes exactly one row
-                P = self.P
-                adam_step_(self.u[:P], self.m[:P], self.v[:P], self.grad[:P],
-                           self.theta[:P] if bnd is not None else None, self.step_dev[0],
-                           self.lr, self.b1, self.b2, self.eps,
-                           None if bnd is None else Bounds(bnd.lo[:P], bnd.hi[:P], bnd.kind[:P]),
-                           self.legacy, traj_base=hb, traj_stride=stride, host_step=self._hstep())
-            else:
-                adam_step_(self.u, self.m, self.v, self.grad,
-                           self.theta if bnd is not None else None, self.step_dev[0],
-                           self.lr, self.b1, self.b2, self.eps, bnd, self.legacy,
-                           traj_base=hb, traj_stride=stride, host_step=self._hstep())
+                with self._ph("grad_allreduce"):
+                    self.comm.all_reduce(self.grad)
+            with self._ph("adam"):
+                self._replicated_adam(hb)
+
+    def _replicated_adam(self, hb):
+        stride = self.P if hb is not None else 0
+        bnd = self.bounds
+        if hb is not None and self.P_pad != self.P:
+            # trajectory rows are P long: update the real parameters and the padding
+            # separately so the kernel writes exactly one row
+            P = self.P
+            adam_step_(self.u[:P], self.m[:P], self.v[:P], self.grad[:P],
+                       self.theta[:P] if bnd is not None else None, self.step_dev[0],
+                       self.lr, self.b1, self.b2, self.eps,
+                       None if bnd is None else Bounds(bnd.lo[:P], bnd.hi[:P], bnd.kind[:P]),
+                       self.legacy, traj_base=hb, traj_stride=stride, host_step=self._hstep())
+        else:
+            adam_step_(self.u, self.m, self.v, self.grad,
+                       self.theta if bnd is not None else None, self.step_dev[0],
+                       self.lr, self.b1, self.b2, self.eps, bnd, self.legacy,
+                       traj_base=hb, traj_stride=stride, host_step=self._hstep())
 
     def _hstep(self):
         """The 0-based step for eager launches; None inside a graph capture (the Adam
