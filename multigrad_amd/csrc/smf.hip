@@ -766,12 +766,53 @@ __global__ __launch_bounds__(kThreads, MG_LANES_MINWAVES) void smf_fwd_lanes_ker
 #ifndef MG_VJP_LANES_PERSIST
 #define MG_VJP_LANES_PERSIST 1
 #endif
-template <int NB, bool LOGSIG>
+// Fused VJP + Adam (unbounded) for shards whose populations are all whole: a lane that
+// has its population's gradient applies the Adam update to the population's (a, s) pair
+// directly -- theta, m, v and the trajectory row -- so the gradient never round-trips
+// through HBM (reference Adam math: multigrad/adam.py:52-68 via jax optimizers.adam; the
+// same expression order as csrc/adam.hip:adam_elem).
+struct VjpAdam {
+  float2* theta;        // parameters (the same array the kernel reads), updated in place
+  float2* m;            // moments, indexed by unit - unit_offset
+  float2* v;
+  float2* traj;         // trajectory base (row r at traj + r * traj_stride floats) or null
+  int64_t traj_stride;  // floats per trajectory row
+  int64_t unit_offset;  // first unit owned by these moment / trajectory arrays
+  const int* step;      // device step counter [step, ticket] (read when host_step < 0)
+  int host_step;
+  float lr, b1, b2, eps;
+};
+
+__device__ __forceinline__ void adam_pair(const VjpAdam& o, float bc1, float bc2, float2 g,
+                                          float2& u, float2& m, float2& v) {
+  m.x = (1.0f - o.b1) * g.x + o.b1 * m.x;
+  m.y = (1.0f - o.b1) * g.y + o.b1 * m.y;
+  v.x = (1.0f - o.b2) * (g.x * g.x) + o.b2 * v.x;
+  v.y = (1.0f - o.b2) * (g.y * g.y) + o.b2 * v.y;
+  u.x = u.x - o.lr * (m.x / bc1) / (sqrtf(v.x / bc2) + o.eps);
+  u.y = u.y - o.lr * (m.y / bc1) / (sqrtf(v.y / bc2) + o.eps);
+}
+
+__global__ void smf_advance_step_kernel(int* step) { step[0] += 1; }
+
+template <int NB, bool LOGSIG, bool ADAM = false>
 __global__ __launch_bounds__(kThreads) void smf_vjp_lanes_kernel(
     const int32_t* __restrict__ slot_pop, const int32_t* __restrict__ slot_part,
-    const float2* __restrict__ theta, const float* __restrict__ hvec,
+    const float2* theta, const float* __restrict__ hvec,  // theta: written back under ADAM
     const float* __restrict__ resid, int64_t s0, int64_t s1,
-    float2* __restrict__ grad, float2* __restrict__ partials) {
+    float2* __restrict__ grad, float2* __restrict__ partials, VjpAdam adam = VjpAdam{}) {
+  float bc1 = 1.0f, bc2 = 1.0f;
+  float2* trow = nullptr;
+  if constexpr (ADAM) {
+    const int st = adam.host_step >= 0
+                       ? adam.host_step
+                       : __hip_atomic_load(adam.step, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    bc1 = 1.0f - powf(adam.b1, (float)(st + 1));
+    bc2 = 1.0f - powf(adam.b2, (float)(st + 1));
+    if (adam.traj)
+      trow = reinterpret_cast<float2*>(reinterpret_cast<float*>(adam.traj) +
+                                       (int64_t)(st + 1) * adam.traj_stride);
+  }
   constexpr int R = 2 * (NB + 1);
   const int lane = threadIdx.x & (kWave - 1);
 #if MG_VJP_LANES_PERSIST
@@ -811,8 +852,21 @@ __global__ __launch_bounds__(kThreads) void smf_vjp_lanes_kernel(
       part = slot_part[gn * kWave + lane];
     }
     if (cc >= 0) {
-      if (pp >= 0) partials[pp] = make_float2(A, B);
-      else grad[cc] = pop_grad<LOGSIG>(theta[cc], A, B);
+      if (pp >= 0) {
+        partials[pp] = make_float2(A, B);
+      } else if constexpr (ADAM) {
+        float2 u = theta[cc];
+        const float2 gr = pop_grad<LOGSIG>(u, A, B);
+        const int64_t j = cc - adam.unit_offset;
+        float2 mm = adam.m[j], vv = adam.v[j];
+        adam_pair(adam, bc1, bc2, gr, u, mm, vv);
+        adam.m[j] = mm;
+        adam.v[j] = vv;
+        adam.theta[cc] = u;  // each lane owns its population's pair
+        if (trow) trow[j] = u;
+      } else {
+        grad[cc] = pop_grad<LOGSIG>(theta[cc], A, B);
+      }
     }
     g = gn;
   }
@@ -1044,6 +1098,73 @@ void smf_vjp(torch::Tensor x, c10::optional<torch::Tensor> pop, torch::Tensor th
     else
       hipLaunchKernelGGL((smf_vjp_finalize_kernel<false>), dim3(ng), dim3(kThreads), 0, stream, giant.data_ptr<int32_t>(), pa, tp, gp);
   }
+}
+
+
+// Fused residual VJP + unbounded Adam over slots [s0, s1) (whole populations only: the
+// caller checks that no split population lies in the range).  m, v (and the optional
+// trajectory rows) cover units [unit_offset, unit_offset + m.numel()/2).
+void smf_vjp_adam_lanes(torch::Tensor slot_pop, torch::Tensor slot_part, torch::Tensor theta,
+                        torch::Tensor h, torch::Tensor resid, int64_t s0, int64_t s1,
+                        std::vector<double> scale, bool log_sigma, torch::Tensor m,
+                        torch::Tensor v, int64_t unit_offset, torch::Tensor step,
+                        int64_t host_step, double lr, double b1, double b2, double eps,
+                        c10::optional<torch::Tensor> traj, int64_t traj_stride) {
+  check_dev(slot_pop, "slot_pop", at::kInt);
+  check_dev(slot_part, "slot_part", at::kInt);
+  check_dev(theta, "theta", at::kFloat);
+  check_dev(h, "h", at::kFloat);
+  check_dev(resid, "resid", at::kFloat);
+  check_dev(m, "m", at::kFloat);
+  check_dev(v, "v", at::kFloat);
+  TORCH_CHECK(step.is_cuda() && step.scalar_type() == at::kInt && step.numel() >= 2, "step: [2] int32 device");
+  const int nbp = padded_bins((int)scale.size());
+  TORCH_CHECK(h.numel() >= nbp + 1, "h too small");
+  const int64_t ns = slot_pop.numel();
+  TORCH_CHECK(slot_part.numel() == ns && resid.dim() == 3 && resid.size(0) * kWave == ns &&
+                  resid.size(1) == 2 * (nbp + 1) && resid.size(2) == kWave && resid.is_contiguous(),
+              "inconsistent residuals");
+  TORCH_CHECK(s0 >= 0 && s1 <= ns && s0 <= s1 && s0 % kWave == 0 && s1 % kWave == 0, "bad slot range");
+  TORCH_CHECK(m.numel() == v.numel() && m.numel() % 2 == 0, "m/v must hold whole units");
+  TORCH_CHECK(unit_offset >= 0 && 2 * (unit_offset + m.numel() / 2) <= theta.numel(), "bad unit offset");
+  VjpAdam a;
+  a.theta = reinterpret_cast<float2*>(theta.data_ptr<float>());
+  a.m = reinterpret_cast<float2*>(m.data_ptr<float>());
+  a.v = reinterpret_cast<float2*>(v.data_ptr<float>());
+  a.traj = nullptr;
+  a.traj_stride = traj_stride;
+  if (traj.has_value() && traj->defined()) {
+    check_dev(*traj, "traj", at::kFloat);
+    TORCH_CHECK(traj_stride % 2 == 0, "trajectory stride must keep float2 alignment");
+    a.traj = reinterpret_cast<float2*>(traj->data_ptr<float>());
+  }
+  a.unit_offset = unit_offset;
+  a.step = step.data_ptr<int>();
+  a.host_step = (int)host_step;
+  a.lr = (float)lr; a.b1 = (float)b1; a.b2 = (float)b2; a.eps = (float)eps;
+  auto stream = at::hip::getCurrentHIPStream();
+  const float2* tp = reinterpret_cast<const float2*>(theta.data_ptr<float>());
+  if (s1 > s0) {
+    int dev = 0, occ = 0;
+    (void)hipGetDevice(&dev);
+    hipDeviceProp_t prop;
+    (void)hipGetDeviceProperties(&prop, dev);
+    MG_DISPATCH_NB(nbp, {
+      (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)smf_vjp_lanes_kernel<NB, true, true>, kThreads, 0);
+    });
+    const int64_t cap = (int64_t)std::max(1, occ) * prop.multiProcessorCount;
+    const int64_t want = (s1 - s0 + kThreads - 1) / kThreads;
+    const int64_t nblk = std::max<int64_t>(kXcds, std::min(cap, want) / kXcds * kXcds);
+    MG_DISPATCH_NB(nbp, {
+      with_bool(log_sigma, [&](auto LS) {
+        hipLaunchKernelGGL((smf_vjp_lanes_kernel<NB, decltype(LS)::value, true>), dim3(nblk), dim3(kThreads), 0,
+                           stream, slot_pop.data_ptr<int32_t>(), slot_part.data_ptr<int32_t>(), tp,
+                           h.data_ptr<float>(), resid.data_ptr<float>(), s0, s1, nullptr, nullptr, a);
+      });
+    });
+  }
+  // graph replays keep the step on the device: advance it once every block has read it
+  if (host_step < 0) hipLaunchKernelGGL(smf_advance_step_kernel, dim3(1), dim3(1), 0, stream, step.data_ptr<int>());
 }
 
 // ------------------------------------------------------------------ lanes host side

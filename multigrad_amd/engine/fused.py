@@ -128,6 +128,7 @@ class FusedAdamEngine:
         self.allow_owner = True if o is None else bool(o)
         self.force_owner = bool(o)
         self.owner = False
+        self.fuse_vjp_adam = bool(_env_flag("MULTIGRAD_FUSED_VJP_ADAM", True))
         nc = chunks if chunks is not None else int(os.environ.get("MULTIGRAD_CHUNKS", "0")) or None
         self.nchunks_req = nc if nc is not None else (1 if self.size == 1 else 4)
         self.comm_ag = None  # second communicator (own RCCL stream) for parameter all-gathers
@@ -151,6 +152,7 @@ class FusedAdamEngine:
             self.use_graph = False
         J, upp = md.engine_units()
         P = J * upp
+        self.upp = upp
         owner_ub = self._owner_units(md, J)
         self.owner = owner_ub is not None
         if self.owner:
@@ -346,7 +348,12 @@ class FusedAdamEngine:
         md = self.model
         self._forward_loss()
         hb = self.history.buf.reshape(-1) if self.history.mode == "full" else None
-        if self.owner:
+        if self.owner and self._fused_vjp_adam(self.rank, self.own_range[0],
+                                               None if self.traj_loc is None
+                                               else self.traj_loc.reshape(-1),
+                                               self.own_range[1] - self.own_range[0]):
+            pass
+        elif self.owner:
             c = self.rank
             with self._ph("vjp"):
                 md.engine_vjp_into(self.theta, self.h, self.grad, chunk=c)
@@ -386,6 +393,8 @@ class FusedAdamEngine:
                 agc = self.comm_ag if self.comm_ag is not None else self.comm
                 self._ag[c] = agc.all_gather_into_tensor(self.theta[pa:pa + L], self.theta[a:b],
                                                          async_op=True)
+        elif self.C == 1 and self._fused_vjp_adam(None, 0, hb, self.P if hb is not None else 0):
+            pass
         else:
             with self._ph("vjp"):
                 for c in range(self.C):
@@ -414,6 +423,17 @@ class FusedAdamEngine:
                        self.theta if bnd is not None else None, self.step_dev[0],
                        self.lr, self.b1, self.b2, self.eps, bnd, self.legacy,
                        traj_base=hb, traj_stride=stride, host_step=self._hstep())
+
+    def _fused_vjp_adam(self, chunk, p0: int, traj, traj_stride: int) -> bool:
+        """Fused VJP + Adam when the gradient is complete locally (owner mode, or one
+        replicated chunk), the parameters are unbounded and the model offers it."""
+        fn = getattr(self.model, "engine_vjp_adam_into", None)
+        if fn is None or not self.fuse_vjp_adam or self.bounds is not None:
+            return False
+        with self._ph("vjp_adam"):
+            return bool(fn(self.theta, self.h, self.m, self.v, p0 // self.upp, self.step_dev[0],
+                           self._hstep(), self.lr, self.b1, self.b2, self.eps, traj_base=traj,
+                           traj_stride=traj_stride, chunk=chunk))
 
     def _hstep(self):
         """The 0-based step for eager launches; None inside a graph capture (the Adam

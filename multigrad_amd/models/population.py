@@ -26,7 +26,7 @@ import torch
 
 from ..ops.smf import (PopulationShard, SmfBins, logmse_loss, prepare_forward, smf_edge_weights_into,
                        smf_forward_into, smf_forward_slab, smf_slab_reduce, smf_sumstats,
-                       smf_vjp_into)
+                       smf_vjp_adam_into, smf_vjp_into)
 from ..parallel.comm import get_world_comm
 from .onepoint import OnePointModel
 
@@ -275,6 +275,14 @@ class PopulationSMFModel(OnePointModel):
     def engine_vjp_into(self, theta, h, grad, chunk=None):
         return smf_vjp_into(theta, self.shard, self.bins, True, h, grad, chunk=chunk,
                             residuals_ready=True, order=self._engine_order())
+
+    def engine_vjp_adam_into(self, theta, h, m, v, unit_offset, step, host_step, lr, b1, b2,
+                             eps, traj_base=None, traj_stride=0, chunk=None) -> bool:
+        """Optional fused VJP + (unbounded) Adam; False where it does not apply."""
+        if self._engine_order() != "internal":
+            return False
+        return smf_vjp_adam_into(theta, self.shard, self.bins, True, h, m, v, unit_offset,
+                                 step, host_step, lr, b1, b2, eps, traj_base, traj_stride, chunk)
 
     # simple (unchunked) protocol helpers
     def engine_partial_into(self, theta, out, slab=None, chunk=None):

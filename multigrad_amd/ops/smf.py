@@ -398,6 +398,32 @@ def prepare_forward(shard: "PopulationShard", bins: SmfBins, log_sigma: bool = T
     shard.wave_schedule(chunk, nblk)
 
 
+def smf_vjp_adam_into(theta: torch.Tensor, shard: "PopulationShard", bins: SmfBins,
+                      log_sigma: bool, h: torch.Tensor, m: torch.Tensor, v: torch.Tensor,
+                      unit_offset: int, step: torch.Tensor, host_step: Optional[int], lr: float,
+                      b1: float, b2: float, eps: float, traj_base: Optional[torch.Tensor] = None,
+                      traj_stride: int = 0, chunk: Optional[int] = None) -> bool:
+    """Fused residual VJP + unbounded Adam (lanes layout, internal order, residuals of a
+    forward at this ``theta``): theta, m, v and the trajectory row of the chunk's units are
+    updated in place and no gradient is materialised.  ``m``/``v`` (and trajectory rows)
+    cover units ``[unit_offset, unit_offset + m.numel() // 2)``.  Returns False (nothing
+    done) where the fused path does not apply: CPU tensors, other layouts, or split
+    populations in the chunk (their gradient needs the cross-part finalize)."""
+    if theta.device.type != "cuda" or shard.layout != "lanes" or shard.resid is None:
+        return False
+    k0, k1 = (0, shard.giant.shape[0]) if chunk is None else \
+        (shard.chunk_giant[chunk], shard.chunk_giant[chunk + 1])
+    if k1 > k0:
+        return False
+    g0, g1 = shard.group_range(chunk)
+    ext().smf_vjp_adam_lanes(shard.slot_index("internal"), shard.slot_part, theta, h,
+                             shard.resid_buffer(bins.nbp), 64 * g0, 64 * g1, list(bins.scale),
+                             bool(log_sigma), m, v, int(unit_offset), step,
+                             -1 if host_step is None else int(host_step), float(lr), float(b1),
+                             float(b2), float(eps), traj_base, int(traj_stride))
+    return True
+
+
 def smf_slab_reduce(slab: torch.Tensor, nrows: int, bins: SmfBins, out: torch.Tensor) -> torch.Tensor:
     """Fixed-order sum of ``nrows`` slab rows per bin, times the bin scale -> ``out``."""
     if slab.device.type != "cuda":

@@ -191,6 +191,26 @@ def test_engine_owner_schedule_single_rank():
         torch.testing.assert_close(eng.params(), t[-1], rtol=0, atol=0)
 
 
+@pytest.mark.parametrize("owner,graph,history", [(False, True, "full"), (False, False, "last"),
+                                                 (True, False, "full"), (True, True, "full")])
+def test_fused_vjp_adam_matches_separate_kernels(owner, graph, history):
+    """The fused VJP + Adam kernel (no gradient in HBM) against the VJP kernel followed by
+    the fused Adam kernel."""
+    from multigrad_amd.engine.fused import FusedAdamEngine
+    from multigrad_amd.models.population import PopulationSMFModel, make_population_data
+    data = make_population_data(num_params=6000, num_halos=300_000, seed=5, device=DEV)
+    model = PopulationSMFModel(aux_data=data)
+    model.set_target_from_truth()
+    sep = FusedAdamEngine(model, graph=graph, owner=owner)
+    sep.fuse_vjp_adam = False
+    ref = sep.run_adam(data["guess"], nsteps=5, learning_rate=1e-3, history=history)
+    eng = FusedAdamEngine(model, graph=graph, owner=owner)
+    assert eng.fuse_vjp_adam
+    t = eng.run_adam(data["guess"], nsteps=5, learning_rate=1e-3, history=history)
+    torch.testing.assert_close(t, ref, rtol=1e-6, atol=1e-7)
+    torch.testing.assert_close(eng.m, sep.m, rtol=1e-5, atol=1e-9)
+
+
 def test_reference_pipeline_on_gpu():
     """Reference tests/test_mpi.py::test_simple_grad_descent_pipeline on the HIP path."""
     from multigrad_amd.models.smf import MySMFModel, ParamTuple, TARGET_SUMSTATS, make_test_data
