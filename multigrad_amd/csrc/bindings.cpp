@@ -32,7 +32,8 @@ void smf_forward_lanes(torch::Tensor xi, torch::Tensor slot_pop, torch::Tensor g
                        torch::Tensor slab, int64_t nblocks, bool rel_tail,
                        c10::optional<torch::Tensor> resid,
                        c10::optional<torch::Tensor> wave_order,
-                       c10::optional<torch::Tensor> wave_start);
+                       c10::optional<torch::Tensor> wave_start,
+                       c10::optional<torch::Tensor> queues);
 void smf_vjp_lanes(torch::Tensor slot_pop, torch::Tensor slot_part, torch::Tensor theta,
                    torch::Tensor h, torch::Tensor resid, int64_t s0, int64_t s1,
                    std::vector<double> scale, bool log_sigma, torch::Tensor grad,
@@ -43,6 +44,7 @@ void smf_vjp_adam_lanes(torch::Tensor slot_pop, torch::Tensor slot_part, torch::
                         torch::Tensor v, int64_t unit_offset, torch::Tensor step,
                         int64_t host_step, double lr, double b1, double b2, double eps,
                         c10::optional<torch::Tensor> traj, int64_t traj_stride);
+torch::Tensor smf_fwd_trace();
 // adam.hip
 void fused_adam(torch::Tensor u, torch::Tensor m, torch::Tensor v, torch::Tensor g,
                 c10::optional<torch::Tensor> p, c10::optional<torch::Tensor> lo,
@@ -83,10 +85,12 @@ PYBIND11_MODULE(_C, m) {
         pybind11::arg("theta"), pybind11::arg("edges"), pybind11::arg("scale"),
         pybind11::arg("log_sigma"), pybind11::arg("g0"), pybind11::arg("g1"), pybind11::arg("slab"),
         pybind11::arg("nblocks"), pybind11::arg("rel_tail"), pybind11::arg("resid") = pybind11::none(),
-        pybind11::arg("wave_order") = pybind11::none(), pybind11::arg("wave_start") = pybind11::none());
+        pybind11::arg("wave_order") = pybind11::none(), pybind11::arg("wave_start") = pybind11::none(),
+        pybind11::arg("queues") = pybind11::none());
   m.def("lpt_waves", &mg::lpt_waves);
   m.def("smf_vjp_lanes", &mg::smf_vjp_lanes);
   m.def("smf_vjp_adam_lanes", &mg::smf_vjp_adam_lanes);
+  m.def("smf_fwd_trace", &mg::smf_fwd_trace);
   m.def("fused_adam", &mg::fused_adam, pybind11::arg("u"), pybind11::arg("m"), pybind11::arg("v"),
         pybind11::arg("g"), pybind11::arg("p"), pybind11::arg("lo"), pybind11::arg("hi"),
         pybind11::arg("kind"), pybind11::arg("step"), pybind11::arg("lr"), pybind11::arg("b1"),

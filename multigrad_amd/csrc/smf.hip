@@ -606,13 +606,21 @@ __device__ __forceinline__ void resid_store(float* p, float v) {
 #endif
 }
 
+// Diagnostics build (-DMG_FWD_TRACE): every wavefront of the lanes forward records its
+// start / end time (s_memrealtime, 100 MHz) and its group count, read back with
+// smf_fwd_trace(); used to split a launch's time into dispatch skew, work and tail.
+#ifdef MG_FWD_TRACE
+constexpr int kTraceWaves = 16384;
+__device__ unsigned long long g_fwd_trace[3 * kTraceWaves];
+#endif
+
 template <int NB, bool LOGSIG, bool REL, bool RESID>
 __global__ __launch_bounds__(kThreads, MG_LANES_MINWAVES) void smf_fwd_lanes_kernel(
     const float* __restrict__ xi, const int32_t* __restrict__ slot_pop,
     const int64_t* __restrict__ group_base, const int32_t* __restrict__ group_len,
     const int32_t* __restrict__ fwd_order, const float2* __restrict__ theta, int64_t g0,
     int64_t g1, SmfBins bins, float* __restrict__ slab, float* __restrict__ resid,
-    const int32_t* __restrict__ wave_start) {
+    const int32_t* __restrict__ wave_start, int* __restrict__ queues, int nq) {
   float acc[NB + 1];
   int cnt[NB + 1];
 #pragma unroll
@@ -643,9 +651,36 @@ __global__ __launch_bounds__(kThreads, MG_LANES_MINWAVES) void smf_fwd_lanes_ker
   // positions [wave_start[w], wave_start[w+1]) of its own list; otherwise positions
   // k in [g0, g1) of the longest-first order, grid-strided.  g = fwd_order[k].
   const int64_t w_id = (int64_t)blockIdx.x * (kThreads / kWave) + wid;
-  int64_t k = wave_start ? (int64_t)wave_start[w_id] : g0 + w_id;
+#ifdef MG_FWD_TRACE
+  const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
+  int n_groups_done = 0;
+#endif
+  // Dynamic (queues != null): nq work queues, queue q holding positions q, q + nq, ... of
+  // the longest-first order; the waves of block b draw from queue b % nq through an atomic
+  // ticket, one group ahead.  Issue arbitration favours the oldest wave of a SIMD, so
+  // waves with equal static loads finish up to 3x apart and the youngest runs the tail
+  // alone (tools/fwd_trace.py); drawing work dynamically lets the fast waves take more.
+  // Every wave makes exactly one failing draw, so draw n_q + waves_q - 1 is the queue's
+  // last of the launch and resets it (graph-replay safe, no extra atomics).
+  const bool dyn = queues != nullptr;
+  const int qid = dyn ? (int)(blockIdx.x % nq) : 0;
+  const int n_items = (int)(g1 - g0);
+  const int n_q = dyn && qid < n_items ? (n_items - qid + nq - 1) / nq : 0;
+  const int waves_q = dyn ? (kThreads / kWave) * (int)((gridDim.x - qid + nq - 1) / nq) : 0;
+  auto draw = [&]() -> int64_t {
+    int t = 0;
+    if (lane == 0) {
+      t = atomicAdd(queues + qid, 1);
+      if (t == n_q + waves_q - 1)
+        __hip_atomic_store(queues + qid, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    t = __builtin_amdgcn_readfirstlane(t);
+    return t < n_q ? g0 + qid + (int64_t)t * nq : g1;
+  };
+  int64_t k = dyn ? draw() : wave_start ? (int64_t)wave_start[w_id] : g0 + w_id;
   const int64_t kstride = wave_start ? 1 : nwaves;
-  if (wave_start) g1 = wave_start[w_id + 1];
+  if (wave_start && !dyn) g1 = wave_start[w_id + 1];
+  int64_t k_next = g1;
   int64_t g = 0;
   float2 th = make_float2(0.f, 0.f);
   const float* xp = xi;
@@ -659,8 +694,8 @@ __global__ __launch_bounds__(kThreads, MG_LANES_MINWAVES) void smf_fwd_lanes_ker
     len = group_len[g];
 #pragma unroll
     for (int u = 0; u < kLanesUnroll; ++u) xn[u] = lane_load(xp, u, len);
-    const int64_t ka = kk + kstride;
-    if (ka < g1) c_next = slot_pop[(int64_t)fwd_order[ka] * kWave + lane];
+    k_next = dyn ? draw() : kk + kstride;
+    if (k_next < g1) c_next = slot_pop[(int64_t)fwd_order[k_next] * kWave + lane];
   };
   if (k < g1) load_group(k, slot_pop[(int64_t)fwd_order[k] * kWave + lane]);
   while (k < g1) {
@@ -711,7 +746,10 @@ __global__ __launch_bounds__(kThreads, MG_LANES_MINWAVES) void smf_fwd_lanes_ker
         lane_halo<NB, LOGSIG, REL, RESID>(xc[u], ninv, mua, bins, acc, cnt, G, W);
 #endif
     }
-    const int64_t kn = k + kstride;
+    const int64_t kn = k_next;
+#ifdef MG_FWD_TRACE
+    ++n_groups_done;
+#endif
     if (kn < g1) load_group(kn, c_next);
     if constexpr (RESID) {  // group-major [g][2 (NB+1)][64]: one contiguous block per group
       float* rg = resid + gc * (2 * (NB + 1) * kWave) + lane;
@@ -747,6 +785,13 @@ __global__ __launch_bounds__(kThreads, MG_LANES_MINWAVES) void smf_fwd_lanes_ker
 #elif MG_LANES_V2
 #pragma unroll
   for (int k = 0; k <= NB; ++k) acc[k] = acc2[k].x + acc2[k].y;
+#endif
+#ifdef MG_FWD_TRACE
+  if (lane == 0 && w_id < kTraceWaves) {
+    g_fwd_trace[3 * w_id] = t_start;
+    g_fwd_trace[3 * w_id + 1] = __builtin_amdgcn_s_memrealtime();
+    g_fwd_trace[3 * w_id + 2] = (unsigned long long)n_groups_done;
+  }
 #endif
   const bool counter = lane == 0;  // the counts are per wave: fold them in once
 #pragma unroll
@@ -1167,6 +1212,17 @@ void smf_vjp_adam_lanes(torch::Tensor slot_pop, torch::Tensor slot_part, torch::
   if (host_step < 0) hipLaunchKernelGGL(smf_advance_step_kernel, dim3(1), dim3(1), 0, stream, step.data_ptr<int>());
 }
 
+torch::Tensor smf_fwd_trace() {
+#ifdef MG_FWD_TRACE
+  auto out = torch::empty({kTraceWaves, 3}, torch::kLong);
+  (void)hipDeviceSynchronize();
+  (void)hipMemcpyFromSymbol(out.data_ptr<int64_t>(), HIP_SYMBOL(g_fwd_trace), sizeof(g_fwd_trace));
+  return out;
+#else
+  return torch::empty({0, 3}, torch::kLong);
+#endif
+}
+
 // ------------------------------------------------------------------ lanes host side
 int64_t smf_fwd_lanes_max_blocks(int64_t nb, bool log_sigma, bool rel_tail, bool resid) {
   const int nbp = padded_bins((int)nb);
@@ -1212,7 +1268,8 @@ void smf_forward_lanes(torch::Tensor xi, torch::Tensor slot_pop, torch::Tensor g
                        torch::Tensor slab, int64_t nblocks, bool rel_tail,
                        c10::optional<torch::Tensor> resid,
                        c10::optional<torch::Tensor> wave_order,
-                       c10::optional<torch::Tensor> wave_start) {
+                       c10::optional<torch::Tensor> wave_start,
+                       c10::optional<torch::Tensor> queues) {
   check_dev(xi, "xi", at::kFloat);
   check_dev(slot_pop, "slot_pop", at::kInt);
   check_dev(group_base, "group_base", at::kLong);
@@ -1248,6 +1305,16 @@ void smf_forward_lanes(torch::Tensor xi, torch::Tensor slot_pop, torch::Tensor g
     order = wave_order->data_ptr<int32_t>();
     ws = wave_start->data_ptr<int32_t>();
   }
+  int* qp = nullptr;
+  int nq = 0;
+  if (queues.has_value() && queues->defined()) {
+    // dynamic schedule over fwd_order[g0, g1); the counters must be 0 (they are left at 0)
+    TORCH_CHECK(!ws, "queues and wave_start are exclusive");
+    check_dev(*queues, "queues", at::kInt);
+    nq = (int)std::min<int64_t>(queues->numel(), nblocks);
+    TORCH_CHECK(nq >= 1, "queues: at least one int32 counter");
+    qp = queues->data_ptr<int>();
+  }
   const SmfBins b = make_bins(edges, scale, nbp);
   auto stream = at::hip::getCurrentHIPStream();
   const float2* tp = reinterpret_cast<const float2*>(theta.data_ptr<float>());
@@ -1257,7 +1324,7 @@ void smf_forward_lanes(torch::Tensor xi, torch::Tensor slot_pop, torch::Tensor g
                          dim3(nblocks), dim3(kThreads), 0, stream, xi.data_ptr<float>(),
                          slot_pop.data_ptr<int32_t>(), group_base.data_ptr<int64_t>(),
                          group_len.data_ptr<int32_t>(), order, tp, g0, g1, b,
-                         slab.data_ptr<float>(), rp, ws);
+                         slab.data_ptr<float>(), rp, ws, qp, nq);
     }); }); });
   });
 }

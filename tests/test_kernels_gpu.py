@@ -299,3 +299,33 @@ def test_lanes_matches_tiles_and_residual_reuse():
     thr2 = th.clone().requires_grad_(True)
     (gk2,) = torch.autograd.grad(S.smf_sumstats(thr2, sl, bins), thr2, torch.ones_like(out))
     assert torch.equal(gk, gk2)
+
+
+def test_forward_schedules_agree(monkeypatch):
+    """Static LPT lists, dynamic work queues (run repeatedly: the kernel must leave its
+    counters at zero) and plain grid-stride give the same sums and residual VJP."""
+    from multigrad_amd.models.population import make_population_data
+    from multigrad_amd.ops import smf as S
+    data = make_population_data(num_params=40_000, num_halos=1_000_000, seed=9, device=DEV)
+    shard, bins = data["shard"], data["bins"]
+    th = data["guess"]
+    h = torch.linspace(0.5, -0.5, bins.nbp + 1, device=DEV)
+    res = {}
+    for mode in ("static", "dynamic", "0"):
+        monkeypatch.setenv("MULTIGRAD_LPT", mode)
+        outs = []
+        for _ in range(3):
+            out = torch.zeros(bins.nbp, device=DEV)
+            S.smf_forward_into(th, shard, bins, True, out, resid=True)
+            grad = torch.zeros_like(th)
+            S.smf_vjp_into(th, shard, bins, True, h, grad, residuals_ready=True)
+            outs.append((out.clone(), grad.clone()))
+        if mode == "dynamic":
+            assert int(shard._queues.abs().sum()) == 0
+        for o, g in outs[1:]:
+            torch.testing.assert_close(o, outs[0][0], rtol=1e-6, atol=0)
+            torch.testing.assert_close(g, outs[0][1], rtol=1e-6, atol=1e-12)
+        res[mode] = outs[0]
+    for mode in ("dynamic", "0"):
+        torch.testing.assert_close(res[mode][0], res["static"][0], rtol=1e-6, atol=0)
+        torch.testing.assert_close(res[mode][1], res["static"][1], rtol=1e-6, atol=1e-12)
