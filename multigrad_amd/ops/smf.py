@@ -323,7 +323,8 @@ class PopulationShard:
             if key not in _GRID_CACHE:
                 _GRID_CACHE[key] = int(ext().smf_fwd_lanes_max_blocks(
                     nbins, bool(log_sigma), bool(rel_tail), True))
-            return int(max(1, min(_GRID_CACHE[key], math.ceil(max(g1 - g0, 1) / 4))))
+            cap = min(_GRID_CACHE[key], int(os.environ.get("MULTIGRAD_FWD_MAX_BLOCKS", "1000000")))
+            return int(max(1, min(cap, math.ceil(max(g1 - g0, 1) / 4))))
         cap = FWD_BLOCKS_MAX
         if self.device.type == "cuda":
             key = (nbins, bool(log_sigma), self.pop is not None, bool(rel_tail))
