@@ -75,6 +75,8 @@ def lbfgs(comm, iters, params, halos):
                                 placement=PLACEMENT)
     m = PopulationSMFModel(aux_data=data, comm=comm)
     m.set_target_from_truth()
+    # warm-up run (first kernel launches load code objects), then a fresh objective
+    lbfgs_minimize(m.fused_engine().lbfgs_objective(data["guess"]), maxiter=2, gtol=0.0, ftol=0.0)
     obj = m.fused_engine().lbfgs_objective(data["guess"])
     _sync(); comm.barrier()
     t0 = time.perf_counter()

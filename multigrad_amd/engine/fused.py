@@ -680,6 +680,12 @@ class _EngineObjective:
             e._ag[c] = agc.all_gather_into_tensor(e.theta[pa:pa + L], e.theta[a:b], async_op=True)
 
     def __call__(self, x: torch.Tensor):
+        loss, g = self.device_call(x)
+        return float(loss.double().item()), g
+
+    def device_call(self, x: torch.Tensor):
+        """``(loss, grad)`` with the loss left on the device (1-element tensor), so the
+        optimizer can fetch it together with its own reductions in one copy."""
         e, md = self.e, self.e.model
         self._load(x)
         e._forward_loss()
@@ -704,7 +710,7 @@ class _EngineObjective:
             if e.size > 1:
                 e.comm.all_reduce(e.grad)
             g = e.grad
-        return float(e.loss.double().item()), g
+        return e.loss, g
 
     def full(self, x: torch.Tensor) -> torch.Tensor:
         """The full parameter vector (model order) for the optimizer's vector x."""

@@ -116,6 +116,9 @@ def lbfgs_minimize(obj, maxiter: int = 100, m: int = 10, ftol: float = 1e7 * _EP
     order: list = []  # ring slots, oldest -> newest
     d = torch.empty_like(x)
     xt = torch.empty_like(x)
+    sy_buf = torch.empty((2, n), dtype=torch.float32, device=dev)  # rows: s_new, y_new
+    dev_call = getattr(obj, "device_call", None) if dev.type == "cuda" else None
+    dot_sy = MultiDot(2, n, dev)
     coef = torch.zeros(2 * m, dtype=torch.float32, device=dev)
 
     def gdot(a: torch.Tensor, b: torch.Tensor) -> float:
@@ -154,12 +157,20 @@ def lbfgs_minimize(obj, maxiter: int = 100, m: int = 10, ftol: float = 1e7 * _EP
 
             def phi(alpha):
                 nonlocal nfev
-                lincomb_(d.view(1, -1), 1, torch.tensor([alpha], dtype=torch.float32, device=dev),
-                         1.0, x, xt)
-                fa, ga = obj(xt)
+                torch.add(x, d, alpha=float(alpha), out=xt)
+                if dev_call is not None:
+                    # loss and the local d.g in ONE device->host copy
+                    lt, ga = dev_call(xt)
+                    ga = ga.clone()
+                    pair = torch.cat([lt.reshape(1).double(), dot1(ga.view(1, -1), 1, [d]).reshape(1)])
+                    fa, da_loc = pair.cpu().numpy()
+                    fa = float(fa)
+                    da = float(_allreduce_np(comm, np.array([da_loc]), sharded=sharded)[0])
+                else:
+                    fa, ga = obj(xt)
+                    ga = ga.clone()
+                    da = gdot(ga, d)
                 nfev += 1
-                ga = ga.clone()
-                da = gdot(ga, d)
                 cache[alpha] = (fa, ga, da)
                 return fa, da
 
@@ -188,12 +199,15 @@ def lbfgs_minimize(obj, maxiter: int = 100, m: int = 10, ftol: float = 1e7 * _EP
                 best = min(cands)[1]
             f_new, g_new, _ = cache[best]
             # ---------------- update iterate and history
-            s_vec = d * best
+            s_vec, y_vec = sy_buf[0], sy_buf[1]
+            torch.mul(d, best, out=s_vec)
             x.add_(s_vec)
-            y_vec = g_new - g
+            torch.sub(g_new, g, out=y_vec)
             nit = k + 1
-            sy_new = gdot(s_vec, y_vec)
-            yy_new = gdot(y_vec, y_vec)
+            # s.y and y.y in one pass and one reduction
+            syy = _allreduce_np(comm, dot_sy(sy_buf, 2, [y_vec]).cpu().numpy().reshape(-1),
+                                sharded=sharded)
+            sy_new, yy_new = float(syy[0]), float(syy[1])
             inserted = sy_new > _EPS * yy_new and yy_new > 0
             if inserted:
                 q = order.pop(0) if len(order) == m else min(set(range(m)) - set(order))
