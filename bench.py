@@ -139,6 +139,9 @@ def main(argv=None):
                                 if engine.owner else "RCCL reduce-scatter + all-gather"
                                 if engine.zero else "RCCL all-reduce" if comm.size > 1
                                 else "none (1 rank)"),
+            "sumstat_allreduce": ("xGMI one-shot kernel (self-tested)"
+                                  if getattr(comm, "_oneshot", None) else
+                                  "RCCL" if comm.size > 1 else "none (1 rank)"),
             "chunks": engine.C,
         },
         "loss_first_timed": loss0,

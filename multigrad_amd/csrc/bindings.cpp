@@ -45,6 +45,14 @@ void smf_vjp_adam_lanes(torch::Tensor slot_pop, torch::Tensor slot_part, torch::
                         int64_t host_step, double lr, double b1, double b2, double eps,
                         c10::optional<torch::Tensor> traj, int64_t traj_stride);
 torch::Tensor smf_fwd_trace();
+// xgmi.hip
+int64_t xgmi_alloc();
+pybind11::bytes xgmi_handle(int64_t base);
+int64_t xgmi_open(pybind11::bytes handle);
+void xgmi_close(int64_t ptr);
+void xgmi_free(int64_t ptr);
+void xgmi_allreduce(torch::Tensor x, std::vector<int64_t> peers, int64_t rank, torch::Tensor seq,
+                    torch::Tensor err, double timeout_s);
 // adam.hip
 void fused_adam(torch::Tensor u, torch::Tensor m, torch::Tensor v, torch::Tensor g,
                 c10::optional<torch::Tensor> p, c10::optional<torch::Tensor> lo,
@@ -91,6 +99,12 @@ PYBIND11_MODULE(_C, m) {
   m.def("smf_vjp_lanes", &mg::smf_vjp_lanes);
   m.def("smf_vjp_adam_lanes", &mg::smf_vjp_adam_lanes);
   m.def("smf_fwd_trace", &mg::smf_fwd_trace);
+  m.def("xgmi_alloc", &mg::xgmi_alloc);
+  m.def("xgmi_handle", &mg::xgmi_handle);
+  m.def("xgmi_open", &mg::xgmi_open);
+  m.def("xgmi_close", &mg::xgmi_close);
+  m.def("xgmi_free", &mg::xgmi_free);
+  m.def("xgmi_allreduce", &mg::xgmi_allreduce);
   m.def("fused_adam", &mg::fused_adam, pybind11::arg("u"), pybind11::arg("m"), pybind11::arg("v"),
         pybind11::arg("g"), pybind11::arg("p"), pybind11::arg("lo"), pybind11::arg("hi"),
         pybind11::arg("kind"), pybind11::arg("step"), pybind11::arg("lr"), pybind11::arg("b1"),

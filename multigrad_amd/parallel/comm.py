@@ -342,6 +342,10 @@ class TorchComm(Comm):
     # ------------------------------------------------------------------ tensors
     def all_reduce(self, tensor, op=SUM, async_op=False):
         c10d = _c10d()
+        if tensor.is_cuda:
+            from .xgmi import maybe_oneshot  # MULTIGRAD_ALLREDUCE=oneshot (opt-in)
+            if maybe_oneshot(self, tensor, op) is not None:
+                return _DoneWork() if async_op else None
         if not tensor.is_contiguous():
             tmp = tensor.contiguous()
             self.all_reduce(tmp, op=op)

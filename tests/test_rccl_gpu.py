@@ -23,7 +23,8 @@ def _rccl_comm():
     return TorchComm(_store(), 0, 1, "WORLD", "w-test", [0], use_device=True)
 
 
-def test_rccl_collectives_single_rank():
+def test_rccl_collectives_single_rank(monkeypatch):
+    monkeypatch.setenv("MULTIGRAD_ALLREDUCE", "rccl")  # tiny all-reduces would go one-shot
     comm = _rccl_comm()
     dev = torch.device("cuda", 0)
     x = torch.arange(8.0, device=dev)

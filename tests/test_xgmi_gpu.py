@@ -1,0 +1,81 @@
+"""One-shot peer-memory all-reduce (csrc/xgmi.hip) with two processes sharing one MI355X:
+IPC export/open of the uncached regions, the flag protocol over many back-to-back calls
+(both slots reused), HIP-graph replay, and the engine with MULTIGRAD_ALLREDUCE=oneshot."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from distributed import run_distributed  # noqa: E402
+
+
+def _protocol(rank, size, ncalls):
+    import multigrad_amd as mg
+    from multigrad_amd.parallel.xgmi import connect
+    comm = mg.get_world_comm()
+    dev = torch.device("cuda", 0)
+    ar = connect(comm, timeout_s=10.0)
+    assert ar is not None
+    g = torch.Generator().manual_seed(100 + rank)
+    vals = [torch.randn(int(n), generator=g) for n in np.arange(ncalls) % 64 + 1]
+    outs = []
+    for v in vals:
+        t = v.to(dev)
+        ar(t)
+        outs.append(t.cpu())
+    # graph replay: the sequence number lives in device memory
+    t = torch.ones(16, device=dev) * (rank + 1)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(graph):
+            ar(t)
+    torch.cuda.current_stream().wait_stream(s)
+    reps = []
+    for _ in range(5):
+        t.fill_(rank + 1.0)
+        graph.replay()
+        reps.append(t.cpu().clone())
+    torch.cuda.synchronize()
+    ok = ar.ok()
+    ar.close()
+    return [v.numpy() for v in vals], [o.numpy() for o in outs], [r.numpy() for r in reps], ok
+
+
+def test_oneshot_protocol_two_procs_one_gpu():
+    res = run_distributed(_protocol, 2, 200, timeout=300)
+    (v0, o0, r0, ok0), (v1, o1, r1, ok1) = res
+    assert ok0 and ok1
+    for a, b, x, y in zip(v0, v1, o0, o1):
+        np.testing.assert_array_equal(x, y)              # identical bits on every rank
+        np.testing.assert_allclose(x, a + b, rtol=1e-6, atol=1e-6)
+    for x, y in zip(r0, r1):
+        np.testing.assert_array_equal(x, np.full(16, 3.0, dtype=np.float32))
+        np.testing.assert_array_equal(y, x)
+
+
+def _engine(rank, size, oneshot):
+    import os
+    os.environ["MULTIGRAD_ALLREDUCE"] = "oneshot" if oneshot else "rccl"
+    import multigrad_amd as mg
+    from multigrad_amd.engine.fused import FusedAdamEngine
+    from multigrad_amd.models.population import PopulationSMFModel, make_population_data
+    comm = mg.get_world_comm()
+    dev = torch.device("cuda", 0)
+    data = make_population_data(6000, 400_000, seed=21, comm=comm, device=dev, placement="owner")
+    model = PopulationSMFModel(aux_data=data, comm=comm)
+    model.set_target_from_truth()
+    eng = FusedAdamEngine(model)
+    traj = eng.run_adam(data["guess"], nsteps=6, learning_rate=1e-3)
+    used = bool(getattr(comm, "_oneshot", None))
+    return traj.cpu().numpy(), used
+
+
+def test_engine_with_oneshot_sumstat_allreduce():
+    ref = run_distributed(_engine, 2, False, timeout=600)
+    res = run_distributed(_engine, 2, True, timeout=600)
+    assert not ref[0][1] and res[0][1] and res[1][1]
+    np.testing.assert_array_equal(res[0][0], res[1][0])
+    np.testing.assert_allclose(res[0][0], ref[0][0], rtol=1e-5, atol=1e-6)
