@@ -33,9 +33,6 @@ namespace mg {
 #ifndef MG_FWD_BALLOT
 #define MG_FWD_BALLOT 1  // integer counts per wave (SALU) instead of per lane (VALU)
 #endif
-#ifndef MG_VJP_EXP
-#define MG_VJP_EXP 0
-#endif
 constexpr int kMaxBins = 32;
 constexpr int kXcds = 8;  // MI355X: 8 XCDs (L2 domains), workgroups dispatched round-robin
 constexpr int kThreads = 256;
@@ -212,16 +209,6 @@ template <int NB, bool LOGSIG>
 __device__ __forceinline__ void halo_vjp(float x, float2 th, float inv, const float (&h)[NB + 1],
                                          const SmfBins& b, float& A, float& B) {
   const float nmi = -(x + th.x) * inv;
-#if MG_VJP_EXP == 2
-  // timing experiment: signed log-weight form (4 VALU/edge); numerically wrong here
-#pragma unroll
-  for (int e = 0; e <= NB; ++e) {
-    const float v = fmaf(b.edge[e], inv, (e & 1) ? -nmi : nmi);
-    const float g = fast_exp2(fmaf(-v, v, h[e]));
-    A = fmaf(b.scale[e & 15], g, A);
-    B = fmaf(g, v, B);
-  }
-#else
 #pragma unroll
   for (int e = 0; e <= NB; ++e) {
     const float w = fmaf(b.edge[e], inv, nmi);
@@ -229,7 +216,6 @@ __device__ __forceinline__ void halo_vjp(float x, float2 th, float inv, const fl
     A += t;
     B = fmaf(t, w, B);
   }
-#endif
 }
 
 // inv is the scaled inverse sigma (kWScale / sigma); A, B from halo_vjp.
@@ -313,11 +299,6 @@ __global__ __launch_bounds__(kThreads) void smf_vjp_tiles_kernel(
     }
   }
   __syncthreads();
-#if MG_VJP_EXP == 1
-  // timing experiment: phase 1 only
-  if (tid < t.p1 - t.p0) grad[t.p0 + tid] = s_ab[tid];
-  return;
-#endif
   // ---- phase 2: blocked per-thread sequential segmented reduction over <= kItems halos
   const int base = tid * kItems;
   const int cnt = (int)max((int64_t)0, min((int64_t)kItems, (t.h1 - t.h0) - base));
@@ -597,9 +578,7 @@ __device__ __forceinline__ float lane_use(float v, int j, int len) {
 #define MG_LANES_NTSTORE 0
 #endif
 __device__ __forceinline__ void resid_store(float* p, float v) {
-#if defined(MG_DBG_NOSTORE)  // timing experiments only: keeps the sums live, drops the stores
-  if (v == 12345.678f) *p = v;
-#elif MG_LANES_NTSTORE
+#if MG_LANES_NTSTORE
   __builtin_nontemporal_store(v, p);
 #else
   *p = v;
