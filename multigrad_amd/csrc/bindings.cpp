@@ -45,6 +45,11 @@ void smf_vjp_adam_lanes(torch::Tensor slot_pop, torch::Tensor slot_part, torch::
                         int64_t host_step, double lr, double b1, double b2, double eps,
                         c10::optional<torch::Tensor> traj, int64_t traj_stride);
 torch::Tensor smf_fwd_trace();
+void smf_epilogue(torch::Tensor slab, int64_t nrows, std::vector<double> edges,
+                  std::vector<double> scale, torch::Tensor target, double eps, torch::Tensor S,
+                  torch::Tensor loss, torch::Tensor h, std::vector<int64_t> peers, int64_t rank,
+                  c10::optional<torch::Tensor> seq, c10::optional<torch::Tensor> err,
+                  double timeout_s);
 // xgmi.hip
 int64_t xgmi_alloc();
 pybind11::bytes xgmi_handle(int64_t base);
@@ -99,6 +104,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("smf_vjp_lanes", &mg::smf_vjp_lanes);
   m.def("smf_vjp_adam_lanes", &mg::smf_vjp_adam_lanes);
   m.def("smf_fwd_trace", &mg::smf_fwd_trace);
+  m.def("smf_epilogue", &mg::smf_epilogue);
   m.def("xgmi_alloc", &mg::xgmi_alloc);
   m.def("xgmi_handle", &mg::xgmi_handle);
   m.def("xgmi_open", &mg::xgmi_open);

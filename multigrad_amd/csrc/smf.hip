@@ -22,6 +22,7 @@
 // sums are combined in a fixed order by a finalize kernel (this is also the path of the
 // 2-parameter shared-parameter models).
 #include "common.h"
+#include "xgmi.h"
 
 #include <torch/extension.h>
 #include <ATen/hip/HIPContext.h>
@@ -200,6 +201,51 @@ __global__ void logmse_loss_kernel(const float* __restrict__ S, const float* __r
     loss[0] = acc / nb;
   }
   if (k <= nb && h) h[k] = edge_weight(g, bins, k, nb);
+}
+
+// Sumstat epilogue of one engine step in ONE launch (one 256-thread workgroup):
+//   slab rows -> local S (fixed-order double sums, bin scale)       [slab_reduce_kernel]
+//   -> cross-rank sum through the one-shot peer-memory exchange      [xgmi.h, size > 1]
+//   -> log-MSE loss and edge weights h (padded edges zeroed)         [logmse_loss_kernel]
+// Replaces three launches and a memset per step (~14 us on an 8-GPU owner shard).
+template <int NB>
+__global__ __launch_bounds__(kThreads) void smf_epilogue_kernel(
+    const float* __restrict__ slab, int nrows, int nb, SmfBins bins, XgmiPeers peers, int rank,
+    int size, unsigned* seq, int* err, long long ticks, const float* __restrict__ target,
+    float eps, float* __restrict__ S_out, float* __restrict__ loss, float* __restrict__ h) {
+  __shared__ double scratch[NB * (kThreads / kWave)];
+  __shared__ float Sv[kXMaxFloats];
+  __shared__ float g[kMaxBins];
+  __shared__ float d2[kMaxBins];
+  double v[NB];
+#pragma unroll
+  for (int k = 0; k < NB; ++k) v[k] = 0.0;
+  for (int r = threadIdx.x; r < nrows; r += kThreads) {
+#pragma unroll
+    for (int k = 0; k < NB; ++k) v[k] += (double)slab[(int64_t)r * NB + k];
+  }
+  block_sum_n<NB>(v, scratch);
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int k = 0; k < NB; ++k) Sv[k] = (float)(v[k] * (double)bins.scale[k]);
+  }
+  __syncthreads();
+  if (size > 1) xgmi_block_allreduce(peers, rank, size, Sv, NB, seq, err, ticks);
+  const int k = threadIdx.x;
+  if (k < NB) S_out[k] = Sv[k];
+  if (k < nb) {
+    const float s = Sv[k] + eps;
+    const float d = log10f(s) - log10f(target[k] + eps);
+    d2[k] = d * d;
+    g[k] = 2.0f / nb * d / (s * kLn10);
+  }
+  __syncthreads();
+  if (k == 0) {
+    float acc = 0.0f;
+    for (int j = 0; j < nb; ++j) acc += d2[j];
+    loss[0] = acc / nb;
+  }
+  if (k <= NB) h[k] = k <= nb ? edge_weight(g, bins, k, nb) : 0.0f;
 }
 
 // Per-halo VJP contributions in the scaled coordinate w = z*kWScale:
@@ -1077,6 +1123,44 @@ void smf_logmse(torch::Tensor S, torch::Tensor target, double eps, std::vector<d
   hipLaunchKernelGGL(logmse_loss_kernel, dim3(1), dim3(64), 0, stream, S.data_ptr<float>(),
                      target.data_ptr<float>(), (float)eps, nb, b, loss.data_ptr<float>(), gp,
                      h.data_ptr<float>());
+}
+
+// Fused sumstat epilogue (see smf_epilogue_kernel); peers empty = single rank.
+void smf_epilogue(torch::Tensor slab, int64_t nrows, std::vector<double> edges,
+                  std::vector<double> scale, torch::Tensor target, double eps, torch::Tensor S,
+                  torch::Tensor loss, torch::Tensor h, std::vector<int64_t> peers, int64_t rank,
+                  c10::optional<torch::Tensor> seq, c10::optional<torch::Tensor> err,
+                  double timeout_s) {
+  check_dev(slab, "slab", at::kFloat);
+  check_dev(target, "target", at::kFloat);
+  check_dev(S, "S", at::kFloat);
+  check_dev(loss, "loss", at::kFloat);
+  check_dev(h, "h", at::kFloat);
+  const int nb = (int)scale.size();
+  const int nbp = padded_bins(nb);
+  TORCH_CHECK(slab.numel() >= nrows * nbp && nrows >= 1, "slab too small");
+  TORCH_CHECK(S.numel() >= nbp && target.numel() >= nb && h.numel() >= nbp + 1, "bad sizes");
+  TORCH_CHECK(nbp <= kXMaxFloats, "too many bins for the one-shot exchange");
+  const int size = peers.empty() ? 1 : (int)peers.size();
+  TORCH_CHECK(size <= kXMaxRanks && rank >= 0 && rank < size, "bad rank/size");
+  XgmiPeers p;
+  for (int r = 0; r < kXMaxRanks; ++r) p.base[r] = r < (int)peers.size() ? reinterpret_cast<char*>(peers[r]) : nullptr;
+  unsigned* sq = nullptr;
+  int* er = nullptr;
+  if (size > 1) {
+    TORCH_CHECK(seq.has_value() && err.has_value(), "multi-rank epilogue needs seq/err");
+    sq = reinterpret_cast<unsigned*>(seq->data_ptr<int>());
+    er = err->data_ptr<int>();
+  }
+  const SmfBins b = make_bins(edges, scale, nbp);
+  auto stream = at::hip::getCurrentHIPStream();
+  const long long ticks = (long long)(timeout_s * 1e8);
+  MG_DISPATCH_NB(nbp, {
+    hipLaunchKernelGGL((smf_epilogue_kernel<NB>), dim3(1), dim3(kThreads), 0, stream,
+                       slab.data_ptr<float>(), (int)nrows, nb, b, p, (int)rank, size, sq, er, ticks,
+                       target.data_ptr<float>(), (float)eps, S.data_ptr<float>(),
+                       loss.data_ptr<float>(), h.data_ptr<float>());
+  });
 }
 
 // VJP over a tile schedule; grad is interleaved [2 * npop]; partials [nslots * 2].

@@ -1,0 +1,70 @@
+// Device side of the one-shot peer-memory all-reduce (see xgmi.hip for the protocol).
+// Shared by the stand-alone all-reduce kernel and by kernels that fuse the exchange into
+// their epilogue (smf.hip: slab reduction -> exchange -> loss in one launch).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+namespace mg {
+
+constexpr int kXMaxRanks = 8;
+constexpr int kXMaxFloats = 64;
+constexpr int kXFlagOff = 0;        // uint32 flags[2][kXMaxRanks]
+constexpr int kXDataOff = 256;      // float data[2][kXMaxRanks][kXMaxFloats]
+constexpr int64_t kXRegionBytes = kXDataOff + 2 * kXMaxRanks * kXMaxFloats * 4;
+
+struct XgmiPeers {
+  char* base[kXMaxRanks];
+};
+
+__device__ __forceinline__ unsigned* xflags(char* b) {
+  return reinterpret_cast<unsigned*>(b + kXFlagOff);
+}
+__device__ __forceinline__ float* xdata(char* b) { return reinterpret_cast<float*>(b + kXDataOff); }
+
+// Block-wide in-place SUM of vals[0..n) (n <= 64; vals in shared or global memory,
+// written by this block) across `size` ranks.  Every thread of the block must call it.
+__device__ __forceinline__ void xgmi_block_allreduce(const XgmiPeers& peers, int rank, int size,
+                                                     float* vals, int n, unsigned* seq_ptr,
+                                                     int* err, long long timeout_ticks) {
+  const int t = threadIdx.x;
+  __syncthreads();
+  const unsigned seq = *seq_ptr + 1u;
+  const int slot = (int)(seq & 1u);
+  if (t < n) {
+    const float mine = vals[t];
+    for (int p = 0; p < size; ++p)
+      __hip_atomic_store(xdata(peers.base[p]) + (slot * kXMaxRanks + rank) * kXMaxFloats + t, mine,
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  __threadfence_system();
+  __syncthreads();
+  if (t < size)
+    __hip_atomic_store(xflags(peers.base[t]) + slot * kXMaxRanks + rank, seq, __ATOMIC_RELEASE,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+  char* me = peers.base[rank];
+  if (t < size) {
+    const long long t0 = wall_clock64();
+    while (__hip_atomic_load(xflags(me) + slot * kXMaxRanks + t, __ATOMIC_ACQUIRE,
+                             __HIP_MEMORY_SCOPE_SYSTEM) != seq) {
+      if (wall_clock64() - t0 > timeout_ticks) {
+        atomicExch(err, 1);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+  }
+  __threadfence_system();
+  __syncthreads();
+  if (t < n) {
+    float s = 0.0f;
+    for (int q = 0; q < size; ++q)
+      s += __hip_atomic_load(xdata(me) + (slot * kXMaxRanks + q) * kXMaxFloats + t,
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    vals[t] = s;
+  }
+  __syncthreads();
+  if (t == 0) *seq_ptr = seq;
+}
+
+}  // namespace mg

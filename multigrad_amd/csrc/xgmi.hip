@@ -23,6 +23,7 @@
 // (multigrad_amd/parallel/xgmi.py; MULTIGRAD_ALLREDUCE=rccl disables it); verified with two
 // processes sharing one GPU (tests/test_xgmi_gpu.py).
 #include "common.h"
+#include "xgmi.h"
 
 #include <torch/extension.h>
 #include <ATen/hip/HIPContext.h>
@@ -33,61 +34,15 @@
 
 namespace mg {
 
-constexpr int kXMaxRanks = 8;
-constexpr int kXMaxFloats = 64;
-constexpr int kXFlagOff = 0;        // uint32 flags[2][kXMaxRanks]
-constexpr int kXDataOff = 256;      // float data[2][kXMaxRanks][kXMaxFloats]
-constexpr int64_t kXRegionBytes = kXDataOff + 2 * kXMaxRanks * kXMaxFloats * 4;
-
-struct XgmiPeers {
-  char* base[kXMaxRanks];
-};
-
-__device__ __forceinline__ unsigned* xflags(char* b) {
-  return reinterpret_cast<unsigned*>(b + kXFlagOff);
-}
-__device__ __forceinline__ float* xdata(char* b) { return reinterpret_cast<float*>(b + kXDataOff); }
-
 __global__ __launch_bounds__(64) void xgmi_oneshot_kernel(XgmiPeers peers, int rank, int size,
                                                          float* __restrict__ x, int n,
                                                          unsigned* __restrict__ seq_ptr,
                                                          int* __restrict__ err,
                                                          long long timeout_ticks) {
-  const int t = threadIdx.x;
-  const unsigned seq = *seq_ptr + 1u;
-  const int slot = (int)(seq & 1u);
-  const float mine = t < n ? x[t] : 0.0f;
-  for (int p = 0; p < size; ++p)
-    if (t < n)
-      __hip_atomic_store(xdata(peers.base[p]) + (slot * kXMaxRanks + rank) * kXMaxFloats + t, mine,
-                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  __threadfence_system();
-  __syncthreads();
-  if (t < size)
-    __hip_atomic_store(xflags(peers.base[t]) + slot * kXMaxRanks + rank, seq, __ATOMIC_RELEASE,
-                       __HIP_MEMORY_SCOPE_SYSTEM);
-  char* me = peers.base[rank];
-  if (t < size) {
-    const long long t0 = wall_clock64();
-    while (__hip_atomic_load(xflags(me) + slot * kXMaxRanks + t, __ATOMIC_ACQUIRE,
-                             __HIP_MEMORY_SCOPE_SYSTEM) != seq) {
-      if (wall_clock64() - t0 > timeout_ticks) {
-        atomicExch(err, 1);
-        break;
-      }
-      __builtin_amdgcn_s_sleep(2);
-    }
-  }
-  __threadfence_system();
-  __syncthreads();
-  if (t < n) {
-    float s = 0.0f;
-    for (int q = 0; q < size; ++q)
-      s += __hip_atomic_load(xdata(me) + (slot * kXMaxRanks + q) * kXMaxFloats + t,
-                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    x[t] = s;
-  }
-  if (t == 0) *seq_ptr = seq;
+  __shared__ float v[kXMaxFloats];
+  if (threadIdx.x < n) v[threadIdx.x] = x[threadIdx.x];
+  xgmi_block_allreduce(peers, rank, size, v, n, seq_ptr, err, timeout_ticks);
+  if (threadIdx.x < n) x[threadIdx.x] = v[threadIdx.x];
 }
 
 static void xcheck(hipError_t e, const char* what) {

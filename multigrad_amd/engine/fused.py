@@ -129,6 +129,9 @@ class FusedAdamEngine:
         self.force_owner = bool(o)
         self.owner = False
         self.fuse_vjp_adam = bool(_env_flag("MULTIGRAD_FUSED_VJP_ADAM", True))
+        # slab reduction (+ one-shot cross-rank sum) + loss in one launch
+        self.fuse_epilogue = bool(_env_flag("MULTIGRAD_FUSED_EPILOGUE", True))
+        self.oneshot = None
         nc = chunks if chunks is not None else int(os.environ.get("MULTIGRAD_CHUNKS", "0")) or None
         self.nchunks_req = nc if nc is not None else (1 if self.size == 1 else 4)
         self.comm_ag = None  # second communicator (own RCCL stream) for parameter all-gathers
@@ -164,6 +167,9 @@ class FusedAdamEngine:
             W = self.size if self.zero else 1
             ub, pb, P_pad, lengths = plan_chunks(J, upp, W, self.nchunks_req)
         md.engine_set_chunks(ub)
+        if self.size > 1 and dev.type == "cuda" and self.fuse_epilogue:
+            from ..parallel.xgmi import get_oneshot
+            self.oneshot = get_oneshot(self.comm)  # collective (all ranks run setup)
         # Internal order: models may keep the engine vectors in their own unit order
         # (e.g. the lanes layout's slot order, for coalesced parameter/gradient access).
         # It must keep every chunk's units inside the chunk, and be the same on all ranks;
@@ -337,6 +343,12 @@ class FusedAdamEngine:
                 self._drain(c)
                 n = md.engine_forward_chunk(self.theta, self.slab[row * self.nS:], c)
                 row += n
+        fused = getattr(md, "engine_reduce_loss_into", None)
+        if fused is not None and self.fuse_epilogue and (self.size == 1 or self.oneshot is not None):
+            with self._ph("sumstat_epilogue"):
+                if fused(self.slab, row, self.S, self.loss, self.h, self.oneshot):
+                    return
+        with self._ph("forward"):
             md.engine_reduce(self.slab, row, self.S)
         if self.size > 1:
             with self._ph("sumstat_allreduce"):

@@ -272,6 +272,25 @@ class PopulationSMFModel(OnePointModel):
         ext().smf_logmse(S_total, t, eps, list(self.bins.edges), list(self.bins.scale),
                          loss_out, self._empty, h_out)
 
+    def engine_reduce_loss_into(self, slab, nrows, S, loss_out, h_out, oneshot=None) -> bool:
+        """Fused epilogue: slab reduction, (with ``oneshot``: the cross-rank sum through
+        the one-shot peer exchange) and loss + edge weights in one launch.  False where it
+        does not apply (CPU), the engine then runs reduce / all-reduce / loss separately."""
+        if slab.device.type != "cuda":
+            return False
+        from ..ops._ext import ext
+        t = self.aux_data["target_sumstats"]
+        if oneshot is None:
+            ext().smf_epilogue(slab, int(nrows), list(self.bins.edges), list(self.bins.scale), t,
+                               float(self.aux_data["loss_eps"]), S, loss_out, h_out, [], 0,
+                               None, None, 5.0)
+        else:
+            ext().smf_epilogue(slab, int(nrows), list(self.bins.edges), list(self.bins.scale), t,
+                               float(self.aux_data["loss_eps"]), S, loss_out, h_out,
+                               oneshot.peers, oneshot.rank, oneshot.seq, oneshot.err,
+                               oneshot.timeout_s)
+        return True
+
     def engine_vjp_into(self, theta, h, grad, chunk=None):
         return smf_vjp_into(theta, self.shard, self.bins, True, h, grad, chunk=chunk,
                             residuals_ready=True, order=self._engine_order())

@@ -24,7 +24,8 @@ import torch
 
 from ..ops._ext import ext
 
-__all__ = ["OneShotAllReduce", "oneshot_enabled", "connect", "MAX_FLOATS", "MAX_RANKS"]
+__all__ = ["OneShotAllReduce", "oneshot_enabled", "connect", "get_oneshot", "MAX_FLOATS",
+           "MAX_RANKS"]
 
 MAX_FLOATS = 64
 MAX_RANKS = 8
@@ -138,3 +139,17 @@ def maybe_oneshot(comm, t: torch.Tensor, op) -> Optional[torch.Tensor]:
     if ar is False:
         return None
     return ar(t)
+
+
+def get_oneshot(comm) -> Optional[OneShotAllReduce]:
+    """The communicator's one-shot context, connecting it now if needed (collective: call
+    on every rank); None when disabled or unavailable (use RCCL)."""
+    if comm is None or comm.size == 1 or not oneshot_enabled() or comm.size > MAX_RANKS:
+        return None
+    if not torch.cuda.is_available():
+        return None
+    ar = getattr(comm, "_oneshot", None)
+    if ar is None:
+        ar = comm._oneshot = connect(
+            comm, float(os.environ.get("MULTIGRAD_ONESHOT_TIMEOUT", "5"))) or False
+    return ar or None

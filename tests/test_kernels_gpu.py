@@ -329,3 +329,22 @@ def test_forward_schedules_agree(monkeypatch):
     for mode in ("dynamic", "0"):
         torch.testing.assert_close(res[mode][0], res["static"][0], rtol=1e-6, atol=0)
         torch.testing.assert_close(res[mode][1], res["static"][1], rtol=1e-6, atol=1e-12)
+
+
+@pytest.mark.parametrize("graph", [False, True])
+def test_fused_epilogue_matches_separate_kernels(graph):
+    """Slab reduction + loss + edge weights in one launch (single rank) against the
+    separate reduce and loss kernels."""
+    from multigrad_amd.engine.fused import FusedAdamEngine
+    from multigrad_amd.models.population import PopulationSMFModel, make_population_data
+    data = make_population_data(num_params=6000, num_halos=300_000, seed=8, device=DEV)
+    model = PopulationSMFModel(aux_data=data)
+    model.set_target_from_truth()
+    sep = FusedAdamEngine(model, graph=graph)
+    sep.fuse_epilogue = False
+    ref = sep.run_adam(data["guess"], nsteps=5, learning_rate=1e-3)
+    eng = FusedAdamEngine(model, graph=graph)
+    t = eng.run_adam(data["guess"], nsteps=5, learning_rate=1e-3)
+    torch.testing.assert_close(t, ref, rtol=1e-6, atol=1e-7)
+    torch.testing.assert_close(eng.loss, sep.loss, rtol=1e-6, atol=0)
+    torch.testing.assert_close(eng.h, sep.h, rtol=1e-6, atol=1e-12)
