@@ -33,7 +33,9 @@ void smf_forward_lanes(torch::Tensor xi, torch::Tensor slot_pop, torch::Tensor g
                        c10::optional<torch::Tensor> resid,
                        c10::optional<torch::Tensor> wave_order,
                        c10::optional<torch::Tensor> wave_start,
-                       c10::optional<torch::Tensor> queues);
+                       c10::optional<torch::Tensor> queues,
+                       c10::optional<std::vector<torch::Tensor>> update,
+                       std::vector<double> update_scalars);
 void smf_vjp_lanes(torch::Tensor slot_pop, torch::Tensor slot_part, torch::Tensor theta,
                    torch::Tensor h, torch::Tensor resid, int64_t s0, int64_t s1,
                    std::vector<double> scale, bool log_sigma, torch::Tensor grad,
@@ -99,7 +101,8 @@ PYBIND11_MODULE(_C, m) {
         pybind11::arg("log_sigma"), pybind11::arg("g0"), pybind11::arg("g1"), pybind11::arg("slab"),
         pybind11::arg("nblocks"), pybind11::arg("rel_tail"), pybind11::arg("resid") = pybind11::none(),
         pybind11::arg("wave_order") = pybind11::none(), pybind11::arg("wave_start") = pybind11::none(),
-        pybind11::arg("queues") = pybind11::none());
+        pybind11::arg("queues") = pybind11::none(), pybind11::arg("update") = pybind11::none(),
+        pybind11::arg("update_scalars") = std::vector<double>());
   m.def("lpt_waves", &mg::lpt_waves);
   m.def("smf_vjp_lanes", &mg::smf_vjp_lanes);
   m.def("smf_vjp_adam_lanes", &mg::smf_vjp_adam_lanes);

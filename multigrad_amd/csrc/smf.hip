@@ -272,6 +272,24 @@ __device__ __forceinline__ float2 pop_grad(float2 th, float A, float B) {
   return make_float2(-inv * A, LOGSIG ? -(kLn10 * kInvW) * B : -(inv * kInvW) * B);
 }
 
+// Pipelined update (see smf_fwd_lanes_kernel<..., UPD>): the previous step's residual
+// VJP + unbounded Adam of a population run in the lane that is about to evaluate the
+// population's halos at the new parameters.
+__global__ void smf_advance_step_kernel(int* step);
+
+struct LanesUpdate {
+  const float* h;       // edge weights of the previous step (NB+1)
+  float2* theta_w;      // parameters, updated in place (same array the kernel reads)
+  float2* m;            // Adam moments, indexed by unit - unit_offset
+  float2* v;
+  float* traj;          // trajectory base or null (row r at traj + r * traj_stride)
+  int64_t traj_stride;
+  int64_t unit_offset;
+  const int* step;      // device step counter (read when host_step < 0)
+  int host_step;
+  float lr, b1, b2, eps;
+};
+
 // Segmented-scan combine: (flag, A, B) pairs.
 struct Seg {
   int f;
@@ -639,13 +657,15 @@ constexpr int kTraceWaves = 16384;
 __device__ unsigned long long g_fwd_trace[3 * kTraceWaves];
 #endif
 
-template <int NB, bool LOGSIG, bool REL, bool RESID>
+template <int NB, bool LOGSIG, bool REL, bool RESID, bool UPD = false>
 __global__ __launch_bounds__(kThreads, MG_LANES_MINWAVES) void smf_fwd_lanes_kernel(
     const float* __restrict__ xi, const int32_t* __restrict__ slot_pop,
     const int64_t* __restrict__ group_base, const int32_t* __restrict__ group_len,
     const int32_t* __restrict__ fwd_order, const float2* __restrict__ theta, int64_t g0,
     int64_t g1, SmfBins bins, float* __restrict__ slab, float* __restrict__ resid,
-    const int32_t* __restrict__ wave_start, int* __restrict__ queues, int nq) {
+    const int32_t* __restrict__ wave_start, int* __restrict__ queues, int nq,
+    LanesUpdate upd = LanesUpdate{}) {
+  static_assert(!UPD || RESID, "the pipelined update reads the residuals it overwrites");
   float acc[NB + 1];
   int cnt[NB + 1];
 #pragma unroll
@@ -711,9 +731,21 @@ __global__ __launch_bounds__(kThreads, MG_LANES_MINWAVES) void smf_fwd_lanes_ker
   const float* xp = xi;
   int len = 0;
   int c_next = 0;
+  int c_cur = -1;
   float xn[kLanesUnroll];
+  float ubc1 = 1.0f, ubc2 = 1.0f;
+  float* utrow = nullptr;
+  if constexpr (UPD) {
+    const int st = upd.host_step >= 0
+                       ? upd.host_step
+                       : __hip_atomic_load(upd.step, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    ubc1 = 1.0f - powf(upd.b1, (float)(st + 1));
+    ubc2 = 1.0f - powf(upd.b2, (float)(st + 1));
+    if (upd.traj) utrow = upd.traj + (int64_t)(st + 1) * upd.traj_stride;
+  }
   auto load_group = [&](int64_t kk, int c) {
     g = fwd_order[kk];
+    c_cur = c;
     th = theta[c < 0 ? 0 : c];
     xp = xi + group_base[g] + lane;
     len = group_len[g];
@@ -725,6 +757,32 @@ __global__ __launch_bounds__(kThreads, MG_LANES_MINWAVES) void smf_fwd_lanes_ker
   if (k < g1) load_group(k, slot_pop[(int64_t)fwd_order[k] * kWave + lane]);
   while (k < g1) {
     const int64_t gc = g;
+    if constexpr (UPD) {
+      // previous step's VJP of this population from its residuals, then Adam: the halos
+      // below are evaluated at the updated parameters
+      const float* rg = resid + gc * (2 * (NB + 1) * kWave) + lane;
+      float A = 0.0f, B = 0.0f;
+#pragma unroll
+      for (int e = 0; e <= NB; ++e) {
+        A = fmaf(upd.h[e], rg[e * kWave], A);
+        B = fmaf(upd.h[e], rg[(NB + 1 + e) * kWave], B);
+      }
+      if (c_cur >= 0) {
+        const float2 gr = pop_grad<LOGSIG>(th, A, B);
+        const int64_t j = c_cur - upd.unit_offset;
+        float2 mm = upd.m[j], vv = upd.v[j];
+        mm.x = (1.0f - upd.b1) * gr.x + upd.b1 * mm.x;
+        mm.y = (1.0f - upd.b1) * gr.y + upd.b1 * mm.y;
+        vv.x = (1.0f - upd.b2) * (gr.x * gr.x) + upd.b2 * vv.x;
+        vv.y = (1.0f - upd.b2) * (gr.y * gr.y) + upd.b2 * vv.y;
+        th.x = th.x - upd.lr * (mm.x / ubc1) / (sqrtf(vv.x / ubc2) + upd.eps);
+        th.y = th.y - upd.lr * (mm.y / ubc1) / (sqrtf(vv.y / ubc2) + upd.eps);
+        upd.m[j] = mm;
+        upd.v[j] = vv;
+        upd.theta_w[c_cur] = th;
+        if (utrow) reinterpret_cast<float2*>(utrow)[j] = th;
+      }
+    }
     const float ninv = -inv_sigma<LOGSIG>(th.y) * kWScale;
     const float mua = -th.x * ninv;
 #if MG_LANES_EP
@@ -1332,7 +1390,9 @@ void smf_forward_lanes(torch::Tensor xi, torch::Tensor slot_pop, torch::Tensor g
                        c10::optional<torch::Tensor> resid,
                        c10::optional<torch::Tensor> wave_order,
                        c10::optional<torch::Tensor> wave_start,
-                       c10::optional<torch::Tensor> queues) {
+                       c10::optional<torch::Tensor> queues,
+                       c10::optional<std::vector<torch::Tensor>> update,
+                       std::vector<double> update_scalars) {
   check_dev(xi, "xi", at::kFloat);
   check_dev(slot_pop, "slot_pop", at::kInt);
   check_dev(group_base, "group_base", at::kLong);
@@ -1381,6 +1441,46 @@ void smf_forward_lanes(torch::Tensor xi, torch::Tensor slot_pop, torch::Tensor g
   const SmfBins b = make_bins(edges, scale, nbp);
   auto stream = at::hip::getCurrentHIPStream();
   const float2* tp = reinterpret_cast<const float2*>(theta.data_ptr<float>());
+  if (update.has_value()) {
+    // pipelined update: tensors [h, m, v, step(int32[2]), traj (or empty)]; scalars
+    // [unit_offset, host_step, lr, b1, b2, eps, traj_stride]
+    const auto& U = *update;
+    TORCH_CHECK(U.size() == 5 && update_scalars.size() == 7, "update: 5 tensors, 7 scalars");
+    TORCH_CHECK(has_resid, "the pipelined update needs the residual buffer");
+    check_dev(U[0], "h", at::kFloat);
+    check_dev(U[1], "m", at::kFloat);
+    check_dev(U[2], "v", at::kFloat);
+    TORCH_CHECK(U[0].numel() >= nbp + 1 && U[1].numel() == U[2].numel(), "bad h/m/v");
+    TORCH_CHECK(U[3].is_cuda() && U[3].scalar_type() == at::kInt, "step: int32 device");
+    LanesUpdate u;
+    u.h = U[0].data_ptr<float>();
+    u.theta_w = reinterpret_cast<float2*>(theta.data_ptr<float>());
+    u.m = reinterpret_cast<float2*>(U[1].data_ptr<float>());
+    u.v = reinterpret_cast<float2*>(U[2].data_ptr<float>());
+    u.traj = U[4].numel() ? U[4].data_ptr<float>() : nullptr;
+    u.unit_offset = (int64_t)update_scalars[0];
+    u.host_step = (int)update_scalars[1];
+    u.lr = (float)update_scalars[2];
+    u.b1 = (float)update_scalars[3];
+    u.b2 = (float)update_scalars[4];
+    u.eps = (float)update_scalars[5];
+    u.traj_stride = (int64_t)update_scalars[6];
+    TORCH_CHECK(u.traj_stride % 2 == 0, "trajectory stride must keep float2 alignment");
+    TORCH_CHECK(u.unit_offset >= 0 && 2 * (u.unit_offset + U[1].numel() / 2) <= theta.numel(),
+                "bad unit offset");
+    u.step = U[3].data_ptr<int>();
+    MG_DISPATCH_NB(nbp, {
+      with_bool(log_sigma, [&](auto LS) { with_bool(rel_tail, [&](auto RT) {
+        hipLaunchKernelGGL((smf_fwd_lanes_kernel<NB, decltype(LS)::value, decltype(RT)::value, true, true>),
+                           dim3(nblocks), dim3(kThreads), 0, stream, xi.data_ptr<float>(),
+                           slot_pop.data_ptr<int32_t>(), group_base.data_ptr<int64_t>(),
+                           group_len.data_ptr<int32_t>(), order, tp, g0, g1, b,
+                           slab.data_ptr<float>(), rp, ws, qp, nq, u);
+      }); });
+    });
+    if (u.host_step < 0) hipLaunchKernelGGL(smf_advance_step_kernel, dim3(1), dim3(1), 0, stream, U[3].data_ptr<int>());
+    return;
+  }
   MG_DISPATCH_NB(nbp, {
     with_bool(log_sigma, [&](auto LS) { with_bool(rel_tail, [&](auto RT) { with_bool(has_resid, [&](auto RS) {
       hipLaunchKernelGGL((smf_fwd_lanes_kernel<NB, decltype(LS)::value, decltype(RT)::value, decltype(RS)::value>),

@@ -139,6 +139,8 @@ class FusedAdamEngine:
         self.use_graph = (self.size == 1) if g is None else bool(g)
         self.graph = None
         self._capturing = False
+        self.pending = False
+        self.pipeline = False
         self.ready = False
         # per-phase HIP-event timing of eager steps (MULTIGRAD_PROFILE=1 or bench.py
         # --profile-phases); never active inside a graph capture
@@ -273,6 +275,13 @@ class FusedAdamEngine:
             if self.comm_ag is None and self.size > 1 and _env_flag("MULTIGRAD_AG_COMM", True):
                 self.comm_ag = self.comm.split(0)
         self._ag: List = [None] * self.C
+        self.pending = False
+        ok = getattr(md, "engine_pipeline_ok", None)
+        self.pipeline = bool(
+            _env_flag("MULTIGRAD_PIPELINE", True) and self.fuse_vjp_adam and bounds is None
+            and (self.owner or (not self.zero and self.C == 1 and self.size == 1))
+            and ok is not None and hasattr(md, "engine_forward_update_chunk")
+            and ok(self.rank if self.owner else None))
         self.graph = None
         self.ready = True
         return self
@@ -331,17 +340,49 @@ class FusedAdamEngine:
         self._ag[c] = None
 
     def drain(self):
+        """Join pending parameter all-gathers and apply a pending (pipelined) update."""
         for c in range(self.C):
             self._drain(c)
+        if self.pending:
+            self.pending = False
+            idx = self.step_host - 1
+            if self.owner:
+                a, b = self.own_range
+                tb = None if self.traj_loc is None else self.traj_loc.reshape(-1)
+                ok = self._fused_vjp_adam(self.rank, a, tb, b - a, host_step=self._hstep(idx))
+            else:
+                hb = self.history.buf.reshape(-1) if self.history.mode == "full" else None
+                ok = self._fused_vjp_adam(None, 0, hb, self.P if hb is not None else 0,
+                                          host_step=self._hstep(idx))
+            assert ok, "pipelined engine lost its fused VJP + Adam path"
 
     # ------------------------------------------------------------------ one step
-    def _forward_loss(self):
+    def _update_args(self, step_idx: int) -> dict:
+        """Arguments of the pending (pipelined) VJP + Adam of step ``step_idx``."""
+        if self.owner:
+            a, b = self.own_range
+            traj = None if self.traj_loc is None else self.traj_loc.reshape(-1)
+            stride = b - a
+        else:
+            a = 0
+            traj = self.history.buf.reshape(-1) if self.history.mode == "full" else None
+            stride = self.P
+        return dict(h=self.h, m=self.m, v=self.v, unit_offset=a // self.upp,
+                    step=self.step_dev[0], host_step=self._hstep(step_idx), lr=self.lr,
+                    b1=self.b1, b2=self.b2, eps=self.eps, traj=traj,
+                    traj_stride=stride if traj is not None else 0)
+
+    def _forward_loss(self, update: bool = False):
         md = self.model
         row = 0
         with self._ph("forward"):
             for c in ([self.rank] if self.owner else range(self.C)):
                 self._drain(c)
-                n = md.engine_forward_chunk(self.theta, self.slab[row * self.nS:], c)
+                if update:  # the previous step's VJP + Adam, fused into this forward
+                    n = md.engine_forward_update_chunk(self.theta, self.slab[row * self.nS:], c,
+                                                       self._update_args(self.step_host - 1))
+                else:
+                    n = md.engine_forward_chunk(self.theta, self.slab[row * self.nS:], c)
                 row += n
         fused = getattr(md, "engine_reduce_loss_into", None)
         if fused is not None and self.fuse_epilogue and (self.size == 1 or self.oneshot is not None):
@@ -358,6 +399,12 @@ class FusedAdamEngine:
 
     def _enqueue_step(self):
         md = self.model
+        if self.pipeline:
+            # step k = [VJP + Adam of step k-1 fused into the forward of step k] + epilogue;
+            # the update of step k stays pending until the next step or drain()
+            self._forward_loss(update=self.pending)
+            self.pending = True
+            return
         self._forward_loss()
         hb = self.history.buf.reshape(-1) if self.history.mode == "full" else None
         if self.owner and self._fused_vjp_adam(self.rank, self.own_range[0],
@@ -436,21 +483,25 @@ class FusedAdamEngine:
                        self.lr, self.b1, self.b2, self.eps, bnd, self.legacy,
                        traj_base=hb, traj_stride=stride, host_step=self._hstep())
 
-    def _fused_vjp_adam(self, chunk, p0: int, traj, traj_stride: int) -> bool:
+    def _fused_vjp_adam(self, chunk, p0: int, traj, traj_stride: int, host_step="auto") -> bool:
         """Fused VJP + Adam when the gradient is complete locally (owner mode, or one
         replicated chunk), the parameters are unbounded and the model offers it."""
         fn = getattr(self.model, "engine_vjp_adam_into", None)
         if fn is None or not self.fuse_vjp_adam or self.bounds is not None:
             return False
         with self._ph("vjp_adam"):
+            hs = self._hstep() if host_step == "auto" else host_step
             return bool(fn(self.theta, self.h, self.m, self.v, p0 // self.upp, self.step_dev[0],
-                           self._hstep(), self.lr, self.b1, self.b2, self.eps, traj_base=traj,
+                           hs, self.lr, self.b1, self.b2, self.eps, traj_base=traj,
                            traj_stride=traj_stride, chunk=chunk))
 
-    def _hstep(self):
-        """The 0-based step for eager launches; None inside a graph capture (the Adam
-        kernel then keeps the step in device memory so the replay self-advances)."""
-        return None if self._capturing else self.step_host
+    def _hstep(self, idx: Optional[int] = None):
+        """The 0-based step for eager launches; None inside a graph capture and for every
+        launch of a graph-mode engine (the Adam kernels then keep the step in device
+        memory, so graph replays and eager launches agree)."""
+        if self._capturing or (self.use_graph and self.pipeline):
+            return None
+        return self.step_host if idx is None else idx
 
     def _capture(self):
         prep = getattr(self.model, "engine_prepare", None)
@@ -472,14 +523,21 @@ class FusedAdamEngine:
         assert self.ready, "call setup() first"
         if self.step_host >= self.nsteps and self.history.mode == "full":
             raise RuntimeError("more steps than the trajectory buffer was sized for")
-        if self.use_graph:
+        if self.use_graph and (self.pending or not self.pipeline):
             if self.graph is None:
                 self._capture()
             self.graph.replay()
+            if self.pipeline:
+                self.pending = True
         else:
             self._enqueue_step()
         self.step_host += 1
         if self.history.mode != "full" and self.traj_loc is None:
+            if self.pipeline:
+                st = self.history.stride
+                if not (self.step_host == self.history.nsteps or
+                        (st and self.step_host % st == 0)):
+                    return
             self.drain()
             if self.owner:
                 st = self.history.stride

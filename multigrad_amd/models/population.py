@@ -252,6 +252,23 @@ class PopulationSMFModel(OnePointModel):
         for c in chunks:
             prepare_forward(self.shard, self.bins, True, c)
 
+    def engine_pipeline_ok(self, chunk=None) -> bool:
+        """Whether :meth:`engine_forward_chunk` can also apply the previous step's VJP and
+        Adam update (lanes layout on the GPU, internal order, no split populations)."""
+        sh = self.shard
+        if sh.device.type != "cuda" or sh.layout != "lanes":
+            return False
+        k0, k1 = (0, sh.giant.shape[0]) if chunk is None else \
+            (sh.chunk_giant[chunk], sh.chunk_giant[chunk + 1])
+        return k1 == k0
+
+    def engine_forward_update_chunk(self, theta, slab, chunk, update: dict) -> int:
+        """Forward of ``chunk`` that first applies the pending VJP + Adam of the previous
+        step per population (``update``: h, m, v, unit_offset, step, host_step, lr, b1, b2,
+        eps, traj, traj_stride) -- one pass instead of a VJP kernel plus a forward."""
+        return smf_forward_slab(theta, self.shard, self.bins, True, slab, chunk, resid=True,
+                                order=self._engine_order(), update=update)
+
     def engine_reduce(self, slab, nrows, S):
         return smf_slab_reduce(slab, nrows, self.bins, S)
 

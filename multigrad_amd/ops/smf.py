@@ -367,7 +367,7 @@ def _user_theta(theta: torch.Tensor, shard: PopulationShard, order: str) -> torc
 
 def smf_forward_slab(theta: torch.Tensor, shard: PopulationShard, bins: SmfBins, log_sigma: bool,
                      slab: torch.Tensor, chunk: Optional[int] = None, resid: bool = False,
-                     order: str = "user") -> int:
+                     order: str = "user", update: Optional[dict] = None) -> int:
     """Forward of the shard (or one population chunk) into per-workgroup slab rows;
     returns the number of rows written.  CPU: one row from the PyTorch reference.
     ``resid`` (lanes layout): also store the VJP residuals of these populations.
@@ -392,10 +392,19 @@ def smf_forward_slab(theta: torch.Tensor, shard: PopulationShard, bins: SmfBins,
         g0, g1 = shard.group_range(chunk)
         rbuf = shard.resid_buffer(bins.nbp) if resid else None
         w_order, w_start, queues = shard.fwd_schedule(chunk, nblk)
+        upd, usc = None, []
+        if update is not None:  # pipelined residual VJP + Adam of the previous step
+            u = update
+            traj = u.get("traj")
+            upd = [u["h"], u["m"], u["v"], u["step"],
+                   traj if traj is not None else torch.empty(0, device=theta.device)]
+            usc = [float(u["unit_offset"]), float(-1 if u.get("host_step") is None else u["host_step"]),
+                   float(u["lr"]), float(u["b1"]), float(u["b2"]), float(u["eps"]),
+                   float(u.get("traj_stride", 0))]
         ext().smf_forward_lanes(shard.xi, shard.slot_index(order), shard.group_base,
                                 shard.group_len, shard.fwd_order, theta, list(bins.edges),
                                 list(bins.scale), bool(log_sigma), g0, g1, slab, nblk,
-                                bins.rel_tail, rbuf, w_order, w_start, queues)
+                                bins.rel_tail, rbuf, w_order, w_start, queues, upd, usc)
         if resid:
             shard.resid_epoch += 1
         return nblk

@@ -348,3 +348,33 @@ def test_fused_epilogue_matches_separate_kernels(graph):
     torch.testing.assert_close(t, ref, rtol=1e-6, atol=1e-7)
     torch.testing.assert_close(eng.loss, sep.loss, rtol=1e-6, atol=0)
     torch.testing.assert_close(eng.h, sep.h, rtol=1e-6, atol=1e-12)
+
+
+@pytest.mark.parametrize("owner,graph,history", [(False, True, "full"), (False, False, "full"),
+                                                 (False, True, "last"), (True, False, "full"),
+                                                 (True, True, 2)])
+def test_pipelined_update_matches_unpipelined(monkeypatch, owner, graph, history):
+    """VJP + Adam of step k fused into the forward of step k+1 (pending until the next
+    step or drain) gives the trajectory of the step-by-step engine; stepping on after a
+    drain (checkpoint) works."""
+    from multigrad_amd.engine.fused import FusedAdamEngine
+    from multigrad_amd.models.population import PopulationSMFModel, make_population_data
+    data = make_population_data(num_params=6000, num_halos=300_000, seed=12, device=DEV)
+    model = PopulationSMFModel(aux_data=data)
+    model.set_target_from_truth()
+    monkeypatch.setenv("MULTIGRAD_PIPELINE", "0")
+    ref_eng = FusedAdamEngine(model, graph=graph, owner=owner)
+    ref = ref_eng.run_adam(data["guess"], nsteps=6, learning_rate=1e-3, history=history)
+    assert not ref_eng.pipeline
+    monkeypatch.setenv("MULTIGRAD_PIPELINE", "1")
+    eng = FusedAdamEngine(model, graph=graph, owner=owner)
+    eng.setup(data["guess"], 6, learning_rate=1e-3, history=history)
+    assert eng.pipeline
+    for i in range(6):
+        eng.step()
+        if i == 2:
+            eng.drain()  # e.g. a checkpoint in the middle
+        torch.testing.assert_close(torch.tensor(eng.last_loss()), torch.tensor(0.0) + eng.last_loss())
+    t = eng.trajectory()
+    torch.testing.assert_close(t, ref, rtol=1e-6, atol=1e-7)
+    torch.testing.assert_close(eng.params(), ref[-1], rtol=1e-6, atol=1e-7)
