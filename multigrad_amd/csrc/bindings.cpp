@@ -51,7 +51,7 @@ void smf_epilogue(torch::Tensor slab, int64_t nrows, std::vector<double> edges,
                   std::vector<double> scale, torch::Tensor target, double eps, torch::Tensor S,
                   torch::Tensor loss, torch::Tensor h, std::vector<int64_t> peers, int64_t rank,
                   c10::optional<torch::Tensor> seq, c10::optional<torch::Tensor> err,
-                  double timeout_s);
+                  double timeout_s, c10::optional<torch::Tensor> advance);
 // xgmi.hip
 int64_t xgmi_alloc();
 pybind11::bytes xgmi_handle(int64_t base);
@@ -107,7 +107,11 @@ PYBIND11_MODULE(_C, m) {
   m.def("smf_vjp_lanes", &mg::smf_vjp_lanes);
   m.def("smf_vjp_adam_lanes", &mg::smf_vjp_adam_lanes);
   m.def("smf_fwd_trace", &mg::smf_fwd_trace);
-  m.def("smf_epilogue", &mg::smf_epilogue);
+  m.def("smf_epilogue", &mg::smf_epilogue, pybind11::arg("slab"), pybind11::arg("nrows"),
+        pybind11::arg("edges"), pybind11::arg("scale"), pybind11::arg("target"), pybind11::arg("eps"),
+        pybind11::arg("S"), pybind11::arg("loss"), pybind11::arg("h"), pybind11::arg("peers"),
+        pybind11::arg("rank"), pybind11::arg("seq"), pybind11::arg("err"), pybind11::arg("timeout_s"),
+        pybind11::arg("advance") = pybind11::none());
   m.def("xgmi_alloc", &mg::xgmi_alloc);
   m.def("xgmi_handle", &mg::xgmi_handle);
   m.def("xgmi_open", &mg::xgmi_open);

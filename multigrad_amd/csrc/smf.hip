@@ -212,7 +212,8 @@ template <int NB>
 __global__ __launch_bounds__(kThreads) void smf_epilogue_kernel(
     const float* __restrict__ slab, int nrows, int nb, SmfBins bins, XgmiPeers peers, int rank,
     int size, unsigned* seq, int* err, long long ticks, const float* __restrict__ target,
-    float eps, float* __restrict__ S_out, float* __restrict__ loss, float* __restrict__ h) {
+    float eps, float* __restrict__ S_out, float* __restrict__ loss, float* __restrict__ h,
+    int* advance) {
   __shared__ double scratch[NB * (kThreads / kWave)];
   __shared__ float Sv[kXMaxFloats];
   __shared__ float g[kMaxBins];
@@ -246,6 +247,9 @@ __global__ __launch_bounds__(kThreads) void smf_epilogue_kernel(
     loss[0] = acc / nb;
   }
   if (k <= NB) h[k] = k <= nb ? edge_weight(g, bins, k, nb) : 0.0f;
+  // the pipelined engine's device step counter, advanced here (the last launch of a step)
+  // instead of by a one-thread kernel of its own
+  if (advance != nullptr && threadIdx.x == 0) advance[0] += 1;
 }
 
 // Per-halo VJP contributions in the scaled coordinate w = z*kWScale:
@@ -614,6 +618,27 @@ __device__ __forceinline__ void lane_halo_ep(float x0, float x1, float ninv, flo
 #endif
 constexpr int kLanesUnroll = MG_LANES_UNROLL;
 
+// MG_LANES_BUF: the lanes kernel addresses xi, slot_pop and the residuals through buffer
+// descriptors (4 SGPRs, rebuilt per group) and one 32-bit lane offset, instead of the 64-bit
+// per-lane pointers the compiler otherwise hoists into VGPR pairs (two VGPRs each): that is
+// what the pipelined-update instantiation needs to stay within 128 VGPRs without spills.
+#ifndef MG_LANES_BUF
+#define MG_LANES_BUF 1
+#endif
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* p) {
+  // raw buffer, stride 0; range 2 GB from the base (every access is base + lane*4 + small)
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, 0x7fffffff, 0x00020000);
+}
+__device__ __forceinline__ float buf_load_f32(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
+}
+__device__ __forceinline__ int buf_load_i32(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+  return (int)__builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0);
+}
+__device__ __forceinline__ void buf_store_f32(__amdgpu_buffer_rsrc_t r, int voff, int soff, float v) {
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, voff, soff, 0);
+}
+
 // Halo j of a lane (sentinel past the end).  MG_LANES_UNCOND: the load itself is
 // unconditional (the host pads xi by 16 rows) and the value is selected, so there is no
 // branch around it and the compiler can count the outstanding loads exactly
@@ -622,6 +647,20 @@ constexpr int kLanesUnroll = MG_LANES_UNROLL;
 #define MG_LANES_UNCOND 0
 #endif
 // (the select happens at the use, lane_use, so the wait lands there and not at the load)
+#if MG_LANES_BUF
+struct LaneSrc {  // this group's halos: descriptor at the group base, lane byte offset
+  __amdgpu_buffer_rsrc_t r;
+  int voff;
+};
+__device__ __forceinline__ float lane_load(const LaneSrc& xp, int j, int len) {
+#if MG_LANES_UNCOND
+  return buf_load_f32(xp.r, xp.voff, j * kWave * 4);
+#else
+  return j < len ? buf_load_f32(xp.r, xp.voff, j * kWave * 4) : kLaneSentinel;
+#endif
+}
+#else
+using LaneSrc = const float*;
 __device__ __forceinline__ float lane_load(const float* xp, int j, int len) {
 #if MG_LANES_UNCOND
   return xp[(int64_t)j * kWave];
@@ -629,6 +668,7 @@ __device__ __forceinline__ float lane_load(const float* xp, int j, int len) {
   return j < len ? xp[(int64_t)j * kWave] : kLaneSentinel;
 #endif
 }
+#endif
 __device__ __forceinline__ float lane_use(float v, int j, int len) {
 #if MG_LANES_UNCOND
   return j < len ? v : kLaneSentinel;
@@ -656,6 +696,36 @@ __device__ __forceinline__ void resid_store(float* p, float v) {
 constexpr int kTraceWaves = 16384;
 __device__ unsigned long long g_fwd_trace[3 * kTraceWaves];
 #endif
+
+// s_waitcnt vmcnt(0) (expcnt / lgkmcnt left alone): global_load_lds writes LDS behind the
+// compiler's back, so its completion is waited for explicitly before the LDS is read.
+__device__ __forceinline__ void vmem_wait_all() { __builtin_amdgcn_s_waitcnt(0x0F70); }
+
+// Wave-wide copy of a contiguous block of NR rows x 64 floats into LDS (global_load_lds:
+// no VGPRs): 1 KB per dwordx4 instruction, then single rows.  One LDS base (M0) per 4 KB,
+// the immediate offset moving both the global and the LDS address.
+template <int I>
+__device__ __forceinline__ void lds_stage_chunk(const float* src, float* dst, int lane) {
+  constexpr int base = (I / 4) * 1024;  // floats
+  __builtin_amdgcn_global_load_lds(src + base + lane * 4, dst + base, 16, (I % 4) * 1024, 0);
+}
+template <int R>
+__device__ __forceinline__ void lds_stage_row(const float* src, float* dst, int lane) {
+  constexpr int base = (R * kWave / 1024) * 1024;
+  __builtin_amdgcn_global_load_lds(src + base + lane, dst + base, 4, (R * kWave - base) * 4, 0);
+}
+template <int NR, int... I, int... R>
+__device__ __forceinline__ void lds_stage_seq(const float* src, float* dst, int lane,
+                                              std::integer_sequence<int, I...>,
+                                              std::integer_sequence<int, R...>) {
+  (lds_stage_chunk<I>(src, dst, lane), ...);
+  (lds_stage_row<(NR / 4) * 4 + R>(src, dst, lane), ...);
+}
+template <int NR>
+__device__ __forceinline__ void lds_stage_block(const float* src, float* dst, int lane) {
+  lds_stage_seq<NR>(src, dst, lane, std::make_integer_sequence<int, NR / 4>{},
+                    std::make_integer_sequence<int, NR % 4>{});
+}
 
 template <int NB, bool LOGSIG, bool REL, bool RESID, bool UPD = false>
 __global__ __launch_bounds__(kThreads, MG_LANES_MINWAVES) void smf_fwd_lanes_kernel(
@@ -728,61 +798,121 @@ __global__ __launch_bounds__(kThreads, MG_LANES_MINWAVES) void smf_fwd_lanes_ker
   int64_t k_next = g1;
   int64_t g = 0;
   float2 th = make_float2(0.f, 0.f);
-  const float* xp = xi;
+#if MG_LANES_BUF
+  const int lane4 = lane * 4;
+  LaneSrc xp{buf_rsrc(xi), lane4};
+  auto slot_of = [&](int64_t kk) {
+    return buf_load_i32(buf_rsrc(slot_pop + (int64_t)fwd_order[kk] * kWave), lane4, 0);
+  };
+#else
+  LaneSrc xp = xi;
+  auto slot_of = [&](int64_t kk) { return slot_pop[(int64_t)fwd_order[kk] * kWave + lane]; };
+#endif
   int len = 0;
   int c_next = 0;
   int c_cur = -1;
   float xn[kLanesUnroll];
-  float ubc1 = 1.0f, ubc2 = 1.0f;
+  float ubc1 = 1.0f, ubc2 = 1.0f;  // UPD: 1 / (1 - b^t)
   float* utrow = nullptr;
   if constexpr (UPD) {
     const int st = upd.host_step >= 0
                        ? upd.host_step
                        : __hip_atomic_load(upd.step, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    ubc1 = 1.0f - powf(upd.b1, (float)(st + 1));
-    ubc2 = 1.0f - powf(upd.b2, (float)(st + 1));
+    // reciprocal bias corrections (uniform): the per-population update below is multiply /
+    // v_rcp / v_sqrt instead of three IEEE divisions per parameter (~30 VALU ops each),
+    // within an ulp or two of the division form (csrc/adam.hip, the stand-alone kernels)
+    ubc1 = 1.0f / (1.0f - powf(upd.b1, (float)(st + 1)));
+    ubc2 = 1.0f / (1.0f - powf(upd.b2, (float)(st + 1)));
     if (upd.traj) utrow = upd.traj + (int64_t)(st + 1) * upd.traj_stride;
   }
-  auto load_group = [&](int64_t kk, int c) {
-    g = fwd_order[kk];
-    c_cur = c;
-    th = theta[c < 0 ? 0 : c];
-    xp = xi + group_base[g] + lane;
-    len = group_len[g];
-#pragma unroll
-    for (int u = 0; u < kLanesUnroll; ++u) xn[u] = lane_load(xp, u, len);
-    k_next = dyn ? draw() : kk + kstride;
-    if (k_next < g1) c_next = slot_pop[(int64_t)fwd_order[k_next] * kWave + lane];
-  };
-  if (k < g1) load_group(k, slot_pop[(int64_t)fwd_order[k] * kWave + lane]);
-  while (k < g1) {
-    const int64_t gc = g;
+  // UPD: the update inputs of a group (its residual block, 1 KB per dwordx4 instruction, and
+  // the lanes' Adam moments) are staged into this wave's LDS slice by global_load_lds when
+  // the group is loaded -- no VGPRs (the 64-bit per-lane pointers of a register load spill
+  // this kernel), and they travel with the theta gather and the first halos, so the group
+  // transition still costs one memory round trip.
+  constexpr int kUR = UPD ? 2 * (NB + 1) + 4 : 1;  // rows: G[NB+1], W[NB+1], m.x m.y v.x v.y
+  float* ubuf = nullptr;
+  const float* uh = nullptr;  // the edge weights, in LDS (a vector load of them would be
+                              // counted by vmcnt and make every group wait for its stores)
+  if constexpr (UPD) {
+    __shared__ __attribute__((aligned(16))) float ub[(kThreads / kWave) * kUR * kWave];
+    __shared__ float hs[NB + 1];
+    if (threadIdx.x <= NB) hs[threadIdx.x] = upd.h[threadIdx.x];
+    __syncthreads();
+    ubuf = ub + wid * (kUR * kWave);
+    uh = hs;
+  }
+  auto stage_update = [&](int64_t gg, int c) {
     if constexpr (UPD) {
-      // previous step's VJP of this population from its residuals, then Adam: the halos
-      // below are evaluated at the updated parameters
-      const float* rg = resid + gc * (2 * (NB + 1) * kWave) + lane;
+      constexpr int NR = 2 * (NB + 1);  // residual rows, contiguous in global memory
+      lds_stage_block<NR>(resid + gg * (NR * kWave), ubuf, lane);
+      const int64_t j = c < 0 ? 0 : c - upd.unit_offset;
+      const float* mp = reinterpret_cast<const float*>(upd.m + j);
+      const float* vp = reinterpret_cast<const float*>(upd.v + j);
+      __builtin_amdgcn_global_load_lds(mp, ubuf + NR * kWave, 4, 0, 0);
+      __builtin_amdgcn_global_load_lds(mp + 1, ubuf + (NR + 1) * kWave, 4, 0, 0);
+      __builtin_amdgcn_global_load_lds(vp, ubuf + (NR + 2) * kWave, 4, 0, 0);
+      __builtin_amdgcn_global_load_lds(vp + 1, ubuf + (NR + 3) * kWave, 4, 0, 0);
+    }
+  };
+  // previous step's VJP of the current group's populations from the staged residuals, then
+  // Adam: the halos are evaluated at the updated parameters
+  auto apply_update = [&]() {
+    if constexpr (UPD) {
+      constexpr int NR = 2 * (NB + 1);
       float A = 0.0f, B = 0.0f;
 #pragma unroll
       for (int e = 0; e <= NB; ++e) {
-        A = fmaf(upd.h[e], rg[e * kWave], A);
-        B = fmaf(upd.h[e], rg[(NB + 1 + e) * kWave], B);
+        A = fmaf(uh[e], ubuf[e * kWave + lane], A);
+        B = fmaf(uh[e], ubuf[(NB + 1 + e) * kWave + lane], B);
       }
       if (c_cur >= 0) {
         const float2 gr = pop_grad<LOGSIG>(th, A, B);
         const int64_t j = c_cur - upd.unit_offset;
-        float2 mm = upd.m[j], vv = upd.v[j];
+        float2 mm = make_float2(ubuf[NR * kWave + lane], ubuf[(NR + 1) * kWave + lane]);
+        float2 vv = make_float2(ubuf[(NR + 2) * kWave + lane], ubuf[(NR + 3) * kWave + lane]);
         mm.x = (1.0f - upd.b1) * gr.x + upd.b1 * mm.x;
         mm.y = (1.0f - upd.b1) * gr.y + upd.b1 * mm.y;
         vv.x = (1.0f - upd.b2) * (gr.x * gr.x) + upd.b2 * vv.x;
         vv.y = (1.0f - upd.b2) * (gr.y * gr.y) + upd.b2 * vv.y;
-        th.x = th.x - upd.lr * (mm.x / ubc1) / (sqrtf(vv.x / ubc2) + upd.eps);
-        th.y = th.y - upd.lr * (mm.y / ubc1) / (sqrtf(vv.y / ubc2) + upd.eps);
+        th.x -= upd.lr * (mm.x * ubc1) * __builtin_amdgcn_rcpf(__builtin_amdgcn_sqrtf(vv.x * ubc2) + upd.eps);
+        th.y -= upd.lr * (mm.y * ubc1) * __builtin_amdgcn_rcpf(__builtin_amdgcn_sqrtf(vv.y * ubc2) + upd.eps);
         upd.m[j] = mm;
         upd.v[j] = vv;
         upd.theta_w[c_cur] = th;
         if (utrow) reinterpret_cast<float2*>(utrow)[j] = th;
       }
     }
+  };
+  auto fetch_next_slot = [&]() {
+    if (k_next < g1) c_next = slot_of(k_next);
+  };
+  auto load_group = [&](int64_t kk, int c, bool fetch_next = true) {
+    g = fwd_order[kk];
+    c_cur = c;
+    stage_update(g, c);
+    th = theta[c < 0 ? 0 : c];
+#if MG_LANES_BUF
+    xp.r = buf_rsrc(xi + group_base[g]);
+#else
+    xp = xi + group_base[g] + lane;
+#endif
+    len = group_len[g];
+#pragma unroll
+    for (int u = 0; u < kLanesUnroll; ++u) xn[u] = lane_load(xp, u, len);
+    k_next = dyn ? draw() : kk + kstride;
+    if (fetch_next) fetch_next_slot();
+  };
+  if (k < g1) {
+    load_group(k, slot_of(k), !UPD);
+    if constexpr (UPD) {
+      vmem_wait_all();
+      apply_update();
+      fetch_next_slot();
+    }
+  }
+  while (k < g1) {
+    const int64_t gc = g;
     const float ninv = -inv_sigma<LOGSIG>(th.y) * kWScale;
     const float mua = -th.x * ninv;
 #if MG_LANES_EP
@@ -833,9 +963,14 @@ __global__ __launch_bounds__(kThreads, MG_LANES_MINWAVES) void smf_fwd_lanes_ker
 #ifdef MG_FWD_TRACE
     ++n_groups_done;
 #endif
-    if (kn < g1) load_group(kn, c_next);
+    if constexpr (!UPD)
+      if (kn < g1) load_group(kn, c_next);
     if constexpr (RESID) {  // group-major [g][2 (NB+1)][64]: one contiguous block per group
+#if MG_LANES_BUF
+      const __amdgpu_buffer_rsrc_t rr = buf_rsrc(resid + gc * (2 * (NB + 1) * kWave));
+#else
       float* rg = resid + gc * (2 * (NB + 1) * kWave) + lane;
+#endif
 #if MG_LANES_EP
       float G[NB + 1], W[NB + 1];
 #pragma unroll
@@ -852,11 +987,27 @@ __global__ __launch_bounds__(kThreads, MG_LANES_MINWAVES) void smf_fwd_lanes_ker
 #endif
 #pragma unroll
       for (int e = 0; e <= NB; ++e) {
+#if MG_LANES_BUF
+        buf_store_f32(rr, lane4, e * kWave * 4, G[e]);
+        buf_store_f32(rr, lane4, (NB + 1 + e) * kWave * 4, W[e]);
+#else
         resid_store(rg + e * kWave, G[e]);
         resid_store(rg + (NB + 1 + e) * kWave, W[e]);
+#endif
       }
     }
     k = kn;
+    // UPD: the next group is loaded after the stores, and everything is waited for before
+    // the staged inputs are read (the compiler does not track global_load_lds): the stores
+    // went out first, so the wait is the one round trip the first halos need anyway
+    if constexpr (UPD) {
+      if (k < g1) {
+        load_group(k, c_next, false);
+        vmem_wait_all();
+        apply_update();
+        fetch_next_slot();  // after the wait: it is not needed before the next transition
+      }
+    }
   }
 #if MG_LANES_EP
 #pragma unroll
@@ -1188,8 +1339,13 @@ void smf_epilogue(torch::Tensor slab, int64_t nrows, std::vector<double> edges,
                   std::vector<double> scale, torch::Tensor target, double eps, torch::Tensor S,
                   torch::Tensor loss, torch::Tensor h, std::vector<int64_t> peers, int64_t rank,
                   c10::optional<torch::Tensor> seq, c10::optional<torch::Tensor> err,
-                  double timeout_s) {
+                  double timeout_s, c10::optional<torch::Tensor> advance) {
   check_dev(slab, "slab", at::kFloat);
+  int* adv = nullptr;
+  if (advance.has_value()) {
+    TORCH_CHECK(advance->is_cuda() && advance->scalar_type() == at::kInt, "advance: int32 device");
+    adv = advance->data_ptr<int>();
+  }
   check_dev(target, "target", at::kFloat);
   check_dev(S, "S", at::kFloat);
   check_dev(loss, "loss", at::kFloat);
@@ -1217,7 +1373,7 @@ void smf_epilogue(torch::Tensor slab, int64_t nrows, std::vector<double> edges,
     hipLaunchKernelGGL((smf_epilogue_kernel<NB>), dim3(1), dim3(kThreads), 0, stream,
                        slab.data_ptr<float>(), (int)nrows, nb, b, p, (int)rank, size, sq, er, ticks,
                        target.data_ptr<float>(), (float)eps, S.data_ptr<float>(),
-                       loss.data_ptr<float>(), h.data_ptr<float>());
+                       loss.data_ptr<float>(), h.data_ptr<float>(), adv);
   });
 }
 
@@ -1445,7 +1601,10 @@ void smf_forward_lanes(torch::Tensor xi, torch::Tensor slot_pop, torch::Tensor g
     // pipelined update: tensors [h, m, v, step(int32[2]), traj (or empty)]; scalars
     // [unit_offset, host_step, lr, b1, b2, eps, traj_stride]
     const auto& U = *update;
-    TORCH_CHECK(U.size() == 5 && update_scalars.size() == 7, "update: 5 tensors, 7 scalars");
+    TORCH_CHECK(U.size() == 5 && (update_scalars.size() == 7 || update_scalars.size() == 8),
+                "update: 5 tensors, 7 scalars (+ defer_advance)");
+    // defer_advance: the caller advances the device step counter itself (the epilogue)
+    const bool defer_advance = update_scalars.size() == 8 && update_scalars[7] != 0.0;
     TORCH_CHECK(has_resid, "the pipelined update needs the residual buffer");
     check_dev(U[0], "h", at::kFloat);
     check_dev(U[1], "m", at::kFloat);
@@ -1478,7 +1637,8 @@ void smf_forward_lanes(torch::Tensor xi, torch::Tensor slot_pop, torch::Tensor g
                            slab.data_ptr<float>(), rp, ws, qp, nq, u);
       }); });
     });
-    if (u.host_step < 0) hipLaunchKernelGGL(smf_advance_step_kernel, dim3(1), dim3(1), 0, stream, U[3].data_ptr<int>());
+    if (u.host_step < 0 && !defer_advance)
+      hipLaunchKernelGGL(smf_advance_step_kernel, dim3(1), dim3(1), 0, stream, U[3].data_ptr<int>());
     return;
   }
   MG_DISPATCH_NB(nbp, {

@@ -375,20 +375,30 @@ class FusedAdamEngine:
     def _forward_loss(self, update: bool = False):
         md = self.model
         row = 0
+        fused = getattr(md, "engine_reduce_loss_into", None)
+        fused_ok = (fused is not None and self.fuse_epilogue
+                    and (self.size == 1 or self.oneshot is not None) and self.slab.is_cuda)
+        advance = None
         with self._ph("forward"):
             for c in ([self.rank] if self.owner else range(self.C)):
                 self._drain(c)
                 if update:  # the previous step's VJP + Adam, fused into this forward
+                    args = self._update_args(self.step_host - 1)
+                    if fused_ok and args["host_step"] is None:
+                        # device step counter: advanced by the epilogue launch, not a kernel
+                        args["defer_advance"] = True
+                        advance = args["step"]
                     n = md.engine_forward_update_chunk(self.theta, self.slab[row * self.nS:], c,
-                                                       self._update_args(self.step_host - 1))
+                                                       args)
                 else:
                     n = md.engine_forward_chunk(self.theta, self.slab[row * self.nS:], c)
                 row += n
-        fused = getattr(md, "engine_reduce_loss_into", None)
-        if fused is not None and self.fuse_epilogue and (self.size == 1 or self.oneshot is not None):
+        if fused_ok:
             with self._ph("sumstat_epilogue"):
-                if fused(self.slab, row, self.S, self.loss, self.h, self.oneshot):
+                if fused(self.slab, row, self.S, self.loss, self.h, self.oneshot,
+                         advance=advance):
                     return
+        assert advance is None, "the step counter advance was deferred to the epilogue"
         with self._ph("forward"):
             md.engine_reduce(self.slab, row, self.S)
         if self.size > 1:

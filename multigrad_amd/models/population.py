@@ -289,10 +289,13 @@ class PopulationSMFModel(OnePointModel):
         ext().smf_logmse(S_total, t, eps, list(self.bins.edges), list(self.bins.scale),
                          loss_out, self._empty, h_out)
 
-    def engine_reduce_loss_into(self, slab, nrows, S, loss_out, h_out, oneshot=None) -> bool:
+    def engine_reduce_loss_into(self, slab, nrows, S, loss_out, h_out, oneshot=None,
+                                advance=None) -> bool:
         """Fused epilogue: slab reduction, (with ``oneshot``: the cross-rank sum through
         the one-shot peer exchange) and loss + edge weights in one launch.  False where it
-        does not apply (CPU), the engine then runs reduce / all-reduce / loss separately."""
+        does not apply (CPU), the engine then runs reduce / all-reduce / loss separately.
+        ``advance``: an int32 device counter the launch increments (the pipelined engine's
+        step counter)."""
         if slab.device.type != "cuda":
             return False
         from ..ops._ext import ext
@@ -300,12 +303,12 @@ class PopulationSMFModel(OnePointModel):
         if oneshot is None:
             ext().smf_epilogue(slab, int(nrows), list(self.bins.edges), list(self.bins.scale), t,
                                float(self.aux_data["loss_eps"]), S, loss_out, h_out, [], 0,
-                               None, None, 5.0)
+                               None, None, 5.0, advance)
         else:
             ext().smf_epilogue(slab, int(nrows), list(self.bins.edges), list(self.bins.scale), t,
                                float(self.aux_data["loss_eps"]), S, loss_out, h_out,
                                oneshot.peers, oneshot.rank, oneshot.seq, oneshot.err,
-                               oneshot.timeout_s)
+                               oneshot.timeout_s, advance)
         return True
 
     def engine_vjp_into(self, theta, h, grad, chunk=None):

@@ -400,7 +400,7 @@ def smf_forward_slab(theta: torch.Tensor, shard: PopulationShard, bins: SmfBins,
                    traj if traj is not None else torch.empty(0, device=theta.device)]
             usc = [float(u["unit_offset"]), float(-1 if u.get("host_step") is None else u["host_step"]),
                    float(u["lr"]), float(u["b1"]), float(u["b2"]), float(u["eps"]),
-                   float(u.get("traj_stride", 0))]
+                   float(u.get("traj_stride", 0)), float(bool(u.get("defer_advance", False)))]
         ext().smf_forward_lanes(shard.xi, shard.slot_index(order), shard.group_base,
                                 shard.group_len, shard.fwd_order, theta, list(bins.edges),
                                 list(bins.scale), bool(log_sigma), g0, g1, slab, nblk,

@@ -374,7 +374,7 @@ def test_pipelined_update_matches_unpipelined(monkeypatch, owner, graph, history
         eng.step()
         if i == 2:
             eng.drain()  # e.g. a checkpoint in the middle
-        torch.testing.assert_close(torch.tensor(eng.last_loss()), torch.tensor(0.0) + eng.last_loss())
+        assert np.isfinite(eng.last_loss())
     t = eng.trajectory()
     torch.testing.assert_close(t, ref, rtol=1e-6, atol=1e-7)
     torch.testing.assert_close(eng.params(), ref[-1], rtol=1e-6, atol=1e-7)
