@@ -10,7 +10,7 @@ Every timed step does the full work of the reference's Adam step
 (multigrad/adam.py:59-66 + multigrad/multigrad.py:508-538): forward over all halos,
 all-reduce of the sumstats, loss + cotangent, VJP over all halos, the cross-rank
 gradient sum, the Adam update of all 1e7 parameters, and the trajectory write of the new
-parameters.  On one GPU the step is a replayed HIP graph.  On N GPUs (one process per
+parameters.  On one GPU the step is two eager launches (pipelined update + epilogue).  On N GPUs (one process per
 GPU, RCCL) the default ``--placement owner`` splits the global catalog by population:
 each rank's gradient is then complete on the populations it owns and zero elsewhere, so
 the per-step collective is the 10-float sumstat all-reduce and every rank updates (and

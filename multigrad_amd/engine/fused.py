@@ -136,6 +136,7 @@ class FusedAdamEngine:
         self.nchunks_req = nc if nc is not None else (1 if self.size == 1 else 4)
         self.comm_ag = None  # second communicator (own RCCL stream) for parameter all-gathers
         g = _env_flag("MULTIGRAD_GRAPH", graph)
+        self._graph_auto = g is None
         self.use_graph = (self.size == 1) if g is None else bool(g)
         self.graph = None
         self._capturing = False
@@ -282,6 +283,10 @@ class FusedAdamEngine:
             and (self.owner or (not self.zero and self.C == 1 and self.size == 1))
             and ok is not None and hasattr(md, "engine_forward_update_chunk")
             and ok(self.rank if self.owner else None))
+        if self._graph_auto:
+            # a pipelined step is two launches (forward+update, epilogue); replaying them
+            # from a graph measured 1-5% slower than eager launches (tools/graph_ab_full.sh)
+            self.use_graph = self.size == 1 and dev.type == "cuda" and not self.pipeline
         self.graph = None
         self.ready = True
         return self
