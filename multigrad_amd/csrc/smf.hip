@@ -597,6 +597,9 @@ __device__ __forceinline__ void lane_halo_ep(float x0, float x1, float ninv, flo
 // Measured on MI355X (1e7 params, 1.34e8 halos, internal order, with residuals): the
 // edge-pair path at 4 waves/SIMD (118 VGPRs, no spills) 595 us vs 615-624 us for the
 // compiler-packed scalar path at 6 waves; at 5 or 6 waves the edge-pair path spills.
+#ifndef MG_FWD_PRIO
+#define MG_FWD_PRIO 1  // static-list issue-priority feedback (tools/ab_prio.sh)
+#endif
 #ifndef MG_LANES_EP
 #define MG_LANES_EP 1
 #endif
@@ -911,7 +914,23 @@ __global__ __launch_bounds__(kThreads, MG_LANES_MINWAVES) void smf_fwd_lanes_ker
       fetch_next_slot();
     }
   }
+#if MG_FWD_PRIO
+  const int64_t k_first = k;
+#endif
   while (k < g1) {
+#if MG_FWD_PRIO
+    // Static lists: the wave's issue priority falls as its list drains, so the SIMD's
+    // arbiter prefers the waves that are behind instead of always the oldest one (which
+    // leaves the youngest wave running the tail alone, profiles/fwd_wave_timeline.md).
+    if (!dyn && wave_start) {
+      const int64_t tot = g1 - k_first;
+      const int lvl = (int)((4 * (g1 - k) - 1) / tot);
+      if (lvl >= 3) __builtin_amdgcn_s_setprio(3);
+      else if (lvl == 2) __builtin_amdgcn_s_setprio(2);
+      else if (lvl == 1) __builtin_amdgcn_s_setprio(1);
+      else __builtin_amdgcn_s_setprio(0);
+    }
+#endif
     const int64_t gc = g;
     const float ninv = -inv_sigma<LOGSIG>(th.y) * kWScale;
     const float mua = -th.x * ninv;

@@ -261,8 +261,13 @@ class PopulationShard:
         (runtime.cpp:lpt_waves); ``dynamic`` -- 256 device work queues drawn by atomic
         tickets (waves that the oldest-first issue arbitration favours take more groups);
         ``0`` -- grid-stride over the longest-first order; ``auto`` (default) -- dynamic
-        when every wave gets >= 8 groups (the tail then shrinks to about one group),
-        static otherwise (measured: 566 vs 579 us at 1.34e8 halos, 98 vs 92 us at 1/8).
+        when every wave gets >= 8 groups, static otherwise.  The static lists run with
+        issue-priority feedback (``MG_FWD_PRIO`` in smf.hip: a wave's priority falls as
+        its list drains), which removes most of the oldest-wave-first tail.  Measured on
+        one MI355X (profiles/fwd_prio_ab.md): kernel alone 543 us static+priority vs
+        551 dynamic at 1.34e8 halos, but the pipelined bench step 0.641 vs 0.636 ms, so
+        dynamic stays at that size; at 1/8 (the 8-GPU owner shard) 0.0993 vs 0.1045 ms
+        per step (0.1086 before the priority feedback).
         """
         mode = os.environ.get("MULTIGRAD_LPT", "auto")
         if mode == "0":
