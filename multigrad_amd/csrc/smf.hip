@@ -923,8 +923,13 @@ __global__ __launch_bounds__(kThreads, MG_LANES_MINWAVES) void smf_fwd_lanes_ker
     // arbiter prefers the waves that are behind instead of always the oldest one (which
     // leaves the youngest wave running the tail alone, profiles/fwd_wave_timeline.md).
     if (!dyn && wave_start) {
+#if MG_FWD_PRIO == 2
+      // longest-remaining-first: priority = groups left after this one (clamped to 3)
+      const int lvl = (int)min((int64_t)3, g1 - k - 1);
+#else
       const int64_t tot = g1 - k_first;
       const int lvl = (int)((4 * (g1 - k) - 1) / tot);
+#endif
       if (lvl >= 3) __builtin_amdgcn_s_setprio(3);
       else if (lvl == 2) __builtin_amdgcn_s_setprio(2);
       else if (lvl == 1) __builtin_amdgcn_s_setprio(1);
