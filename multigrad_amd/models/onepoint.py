@@ -204,14 +204,28 @@ class OnePointModel(_OptimizerFrontEnds):
         if self.comm is not None and self.comm.size > 1:
             params = self.comm.bcast(params, root=0)
         rk = _rk(randkey)
+        # all partial sumstats first, then ONE all-reduce of the stacked [num_eval, ...]
+        # tensor instead of one small collective per evaluation (reference
+        # multigrad/multigrad.py:354-388 reduces inside the loop)
+        partials, auxes = [], []
+        with torch.no_grad():
+            for x in params:
+                r = self.calc_partial_sumstats_from_params(self._params(x), **rk)
+                a = None
+                if self.sumstats_func_has_aux:
+                    r, a = r
+                partials.append(torch.as_tensor(r))
+                auxes.append(a)
+        if not partials:
+            return params, np.array([]), np.array([])
+        totals = self._allreduce(torch.stack(partials))
         sumstats, losses = [], []
-        for x in params:
-            s = self.calc_sumstats_from_params(x, **rk)
-            args = s if self.sumstats_func_has_aux else (s,)
+        for s, a in zip(totals, auxes):
+            args = (s, a) if self.sumstats_func_has_aux else (s,)
             loss = self.calc_loss_from_sumstats(*args, **rk)
             if self.loss_func_has_aux:
                 loss = loss[0]
-            sumstats.append(np.asarray((s[0] if self.sumstats_func_has_aux else s).cpu()))
+            sumstats.append(np.asarray(s.cpu()))
             losses.append(float(loss))
         return params, np.array(sumstats), np.array(losses)
 

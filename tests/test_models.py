@@ -155,6 +155,10 @@ def test_onepointgroup_sums_subcomm_models():
 def _lhs_body(rank, size):
     m = SumOfSquaresModel(aux_data=make_toy_data(ndim=2, npoints=30, seed=1))
     params, sumstats, losses = m.run_lhs_param_scan([-1, -2], [1, 2], 2, 6, seed=None)
+    # the scan's single batched all-reduce matches per-point evaluation
+    for x, s, l in zip(params, sumstats, losses):
+        np.testing.assert_allclose(s, m.calc_sumstats_from_params(x).numpy(), rtol=1e-6)
+        assert l == pytest.approx(float(m.calc_loss_from_params(x)), rel=1e-6)
     return params.tolist(), sumstats.tolist(), losses.tolist()
 
 
