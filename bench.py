@@ -10,31 +10,39 @@ Every timed step does the full work of the reference's Adam step
 (multigrad/adam.py:59-66 + multigrad/multigrad.py:508-538): forward over all halos,
 all-reduce of the sumstats, loss + cotangent, VJP over all halos, the cross-rank
 gradient sum, the Adam update of all 1e7 parameters, and the trajectory write of the new
-parameters.  On one GPU the step is two eager launches (pipelined update + epilogue).  On N GPUs (one process per
-GPU, RCCL) the default ``--placement owner`` splits the global catalog by population:
-each rank's gradient is then complete on the populations it owns and zero elsewhere, so
-the per-step collective is the 10-float sumstat all-reduce and every rank updates (and
-records the trajectory of) only its own parameters.  ``--placement hashed`` splits the
-catalog by halo index instead: every rank's gradient is dense and the engine runs a
-chunked RCCL reduce-scatter (overlapped with the VJP), Adam on each rank's 1/N slice and
-an in-place all-gather (ZeRO-1) -- the same bytes as one all-reduce.  Both placements
-hold the same global data set and give the same trajectory (tests/test_engine.py).
+parameters.
 
-Usage: ``python bench.py [--gpus N] [--steps K] [--warmup W]``; for N>1 launch with
-``python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py``.
+On N > 1 GPUs (one process per GPU) two placements of the same global catalog are timed
+back to back in one run:
+
+* ``value`` -- **hashed** placement, the reference's data parallelism (BASELINE config 3,
+  reference multigrad/multigrad.py:522,531-532): every rank holds a contiguous block of
+  halo indices, so every rank's gradient is dense over all 1e7 parameters and the engine
+  sums it across ranks every step (reduce-scatter -> Adam on the owned 1/N slice ->
+  all-gather, ZeRO-1; the same bytes as one all-reduce).
+* ``owner_steps_per_s`` -- **owner** placement: the catalog is split by population, each
+  rank's gradient is complete on the populations it owns, and the per-step collective is
+  the 10-float sumstat all-reduce only.
+
+Usage: ``python bench.py [--gpus N] [--steps K] [--warmup W]``.  With ``--gpus N > 1`` and no
+launcher environment the script starts ``torch.distributed.run`` with N ranks itself
+(before any GPU call in this process) and relays rank 0's JSON line; under a launcher
+(``WORLD_SIZE`` set) it runs as one rank.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
 os.environ.setdefault("MULTIGRAD_PROGRESS", "0")
 
 
-def main(argv=None):
+def _args(argv=None):
     ap = argparse.ArgumentParser(description=__doc__)
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
@@ -44,43 +52,57 @@ def main(argv=None):
                     help="global number of halos (fixed across GPU counts: strong scaling)")
     ap.add_argument("--lr", type=float, default=1e-3)
     ap.add_argument("--history", default="full", help="trajectory: full | last | <stride>")
-    ap.add_argument("--placement", default="owner", choices=["owner", "hashed"],
-                    help="halo -> rank placement for N > 1: 'owner' splits the catalog by "
-                         "population (gradient shards complete on their owner, no gradient "
-                         "collective); 'hashed' splits it by halo index (dense gradient, "
-                         "ZeRO reduce-scatter + all-gather every step)")
+    ap.add_argument("--placement", default="both", choices=["both", "hashed", "owner"],
+                    help="halo -> rank placement timed for N > 1: 'hashed' (dense gradient "
+                         "summed across ranks every step: the headline value), 'owner' "
+                         "(catalog split by population), or 'both' (default: hashed is "
+                         "'value', owner is 'owner_steps_per_s')")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--profile-phases", action="store_true")
-    args = ap.parse_args(argv)
+    return ap.parse_args(argv)
 
+
+def _free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return int(s.getsockname()[1])
+
+
+def launch(args, argv) -> int:
+    """Start ``args.gpus`` ranks with torch.distributed.run and relay their output.
+
+    Runs in a process that has made no GPU call (device counting does not initialise
+    the runtime), and starts the ranks as children -- never exec."""
     import torch
-    import multigrad_amd as mg
+    ndev = torch.cuda.device_count()
+    if 0 < ndev < args.gpus:
+        print(f"bench.py: --gpus {args.gpus} requested but only {ndev} GPU(s) are visible",
+              file=sys.stderr, flush=True)
+        return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr", "127.0.0.1",
+           "--master-port", str(_free_port()), os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "1")
+    return subprocess.run(cmd, env=env).returncode
+
+
+def time_placement(placement, args, comm, dev, sync):
+    """Build the data and engine for one placement, warm up, time ``args.steps`` steps.
+
+    Returns the per-rank record (elapsed is the MAX over ranks)."""
+    import torch
     from multigrad_amd.models.population import PopulationSMFModel, make_population_data
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    if world > 1:
-        comm = mg.init_distributed()
-    else:
-        comm = mg.get_world_comm()
-    if torch.cuda.is_available():
-        torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")) % torch.cuda.device_count())
-    # CPU fallback (PyTorch reference math) only so the JSON contract is testable without a
-    # GPU; every measured number comes from the HIP path
-    dev = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() \
-        else torch.device("cpu")
-
-    def sync():
-        if dev.type == "cuda":
-            torch.cuda.synchronize()
 
     t_setup = time.perf_counter()
     data = make_population_data(args.params, args.halos, seed=1234, comm=comm, device=dev,
-                                placement=args.placement if comm.size > 1 else "hashed")
+                                placement=placement if comm.size > 1 else "hashed")
     model = PopulationSMFModel(aux_data=data, comm=comm)
     model.set_target_from_truth()
     history = args.history if args.history in ("full", "last") else int(args.history)
     engine = model.fused_engine(graph=False if (args.no_graph or args.profile_phases) else None)
-    if args.profile_phases:  # HIP-event timing per phase (eager launches; stderr summary)
+    if args.profile_phases:  # HIP-event timing per phase (eager launches)
         from multigrad_amd.utils.profiling import PhaseTimer
         engine.timer = PhaseTimer(True)
     engine.setup(data["guess"], nsteps=args.warmup + args.steps, learning_rate=args.lr,
@@ -97,59 +119,123 @@ def main(argv=None):
     t0 = time.perf_counter()
     for _ in range(args.steps):
         engine.step()
-    engine.drain()  # last all-gathers joined into the compute stream
+    engine.drain()  # the pipelined last update / last all-gathers are inside the timing
     sync()
     comm.barrier()
     elapsed = time.perf_counter() - t0
+    engine.check()  # a failed peer exchange raises here instead of reporting wrong numbers
     loss1 = engine.last_loss()
     if comm.size > 1:
         t = torch.tensor([elapsed], dtype=torch.float64)
         comm.all_reduce(t, op="max")
         elapsed = float(t.item())
+    info = {
+        "elapsed": elapsed,
+        "steps_per_s": args.steps / elapsed,
+        "ms_per_step": 1e3 * elapsed / args.steps,
+        "parallelism": f"dp{comm.size}" + ("-owner" if engine.owner else ""),
+        "graph": bool(engine.use_graph),
+        "pipelined": bool(engine.pipeline),
+        "optimizer_sharding": ("owner" if engine.owner else "zero1" if engine.zero
+                               else "replicated"),
+        "placement": data["placement"],
+        "grad_collective": engine.grad_collective_name(),
+        "sumstat_allreduce": engine.sumstat_collective_name(),
+        "chunks": engine.C,
+        "loss_first_timed": loss0,
+        "loss_last": loss1,
+        "setup_s": round(setup_s, 2),
+        "history": history,
+    }
+    if args.profile_phases:
+        info["phases_ms"] = {k: round(v, 4) for k, v in engine.timer.summary().items()}
+    del engine, model, data
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+    return info
 
-    sps = args.steps / elapsed
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else list(argv)
+    args = _args(argv)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return launch(args, argv)
+
+    import torch
+    import multigrad_amd as mg
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    comm = mg.init_distributed() if world > 1 else mg.get_world_comm()
+    if comm.size != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started "
+                         f"{comm.size} rank(s)")
+    if torch.cuda.is_available():
+        torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")) % torch.cuda.device_count())
+    # CPU fallback (PyTorch reference math) only so the JSON contract is testable without a
+    # GPU; every measured number comes from the HIP path
+    dev = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() \
+        else torch.device("cpu")
+
+    def sync():
+        if dev.type == "cuda":
+            torch.cuda.synchronize()
+
+    if comm.size == 1:
+        order = ["hashed"]  # one rank: the placements coincide
+    elif args.placement == "both":
+        order = ["hashed", "owner"]
+    else:
+        order = [args.placement]
+    res = {p: time_placement(p, args, comm, dev, sync) for p in order}
+    head = res[order[0]]
+    own = res.get("owner", head if comm.size == 1 else None)
+    history = head["history"]
     rec = {
         "metric": "Adam steps/sec (whole node), 1e7-param summed-loss model",
-        "value": round(sps, 3),
+        "value": round(head["steps_per_s"], 3),
         "unit": "steps/s",
         "n_gpus": comm.size,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": round(1e3 * elapsed / args.steps, 4),
+        "ms_per_step": round(head["ms_per_step"], 4),
         "higher_is_better": True,
         "scaling": "strong",
         "vs_baseline": None,
         "dtype": "fp32",
-        "data": "synthetic",
+        "data": "synthetic (counter-hash halo catalog, random-init truth parameters)",
         "config": {
             "model": f"population-SMF summed-loss model, {args.params:.0e} params "
                      f"({args.params // 2} populations x (a, log10 sigma)), 10 bins, log-MSE",
             "global_batch": args.halos,
             "seq_len": 10,
-            "parallelism": f"dp{comm.size}" + ("-owner" if engine.owner else ""),
+            "parallelism": head["parallelism"],
             "params": args.params,
             "halos_global": args.halos,
             "optimizer": "Adam (fused HIP kernel), full trajectory" if history == "full"
                          else f"Adam (fused HIP kernel), history={history}",
-            "graph": bool(engine.use_graph),
-            "optimizer_sharding": ("owner" if engine.owner else "zero1" if engine.zero
-                                   else "replicated"),
-            "placement": data["placement"],
-            "grad_collective": ("none: owner-local gradients, sumstat all-reduce only"
-                                if engine.owner else "RCCL reduce-scatter + all-gather"
-                                if engine.zero else "RCCL all-reduce" if comm.size > 1
-                                else "none (1 rank)"),
-            "sumstat_allreduce": ("xGMI one-shot kernel (self-tested)"
-                                  if getattr(comm, "_oneshot", None) else
-                                  "RCCL" if comm.size > 1 else "none (1 rank)"),
-            "chunks": engine.C,
+            "graph": head["graph"],
+            "pipelined": head["pipelined"],
+            "optimizer_sharding": head["optimizer_sharding"],
+            "placement": head["placement"],
+            "grad_collective": head["grad_collective"],
+            "sumstat_allreduce": head["sumstat_allreduce"],
+            "chunks": head["chunks"],
         },
-        "loss_first_timed": loss0,
-        "loss_last": loss1,
-        "setup_s": round(setup_s, 2),
+        "owner_steps_per_s": None if own is None else round(own["steps_per_s"], 3),
+        "owner_ms_per_step": None if own is None else round(own["ms_per_step"], 4),
+        "loss_first_timed": head["loss_first_timed"],
+        "loss_last": head["loss_last"],
+        "setup_s": head["setup_s"],
     }
+    if own is not None and own is not head:
+        rec["owner_config"] = {k: own[k] for k in ("parallelism", "optimizer_sharding",
+                                                   "grad_collective", "sumstat_allreduce",
+                                                   "chunks", "pipelined")}
     if args.profile_phases:
-        rec["phases_ms"] = {k: round(v, 4) for k, v in engine.timer.summary().items()}
+        rec["phases_ms"] = head["phases_ms"]
+        if own is not None and own is not head:
+            rec["owner_phases_ms"] = own["phases_ms"]
     if comm.rank == 0:
         print(json.dumps(rec), flush=True)
     if comm.size > 1:
@@ -157,7 +243,8 @@ def main(argv=None):
         import torch.distributed as dist
         if dist.is_initialized():
             dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -57,6 +57,7 @@ int64_t xgmi_alloc();
 pybind11::bytes xgmi_handle(int64_t base);
 int64_t xgmi_open(pybind11::bytes handle);
 void xgmi_close(int64_t ptr);
+void xgmi_zero(int64_t base);
 void xgmi_free(int64_t ptr);
 void xgmi_allreduce(torch::Tensor x, std::vector<int64_t> peers, int64_t rank, torch::Tensor seq,
                     torch::Tensor err, double timeout_s);
@@ -116,6 +117,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("xgmi_handle", &mg::xgmi_handle);
   m.def("xgmi_open", &mg::xgmi_open);
   m.def("xgmi_close", &mg::xgmi_close);
+  m.def("xgmi_zero", &mg::xgmi_zero);
   m.def("xgmi_free", &mg::xgmi_free);
   m.def("xgmi_allreduce", &mg::xgmi_allreduce);
   m.def("fused_adam", &mg::fused_adam, pybind11::arg("u"), pybind11::arg("m"), pybind11::arg("v"),

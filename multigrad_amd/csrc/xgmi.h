@@ -43,12 +43,19 @@ __device__ __forceinline__ void xgmi_block_allreduce(const XgmiPeers& peers, int
     __hip_atomic_store(xflags(peers.base[t]) + slot * kXMaxRanks + rank, seq, __ATOMIC_RELEASE,
                        __HIP_MEMORY_SCOPE_SYSTEM);
   char* me = peers.base[rank];
+  // a peer that never signals (a rank that skipped the call, or is late by more than the
+  // timeout) must not yield a silently wrong sum: the error word is raised for the host
+  // (checked at the engine's sync points) and the result is poisoned with NaN
+  __shared__ int timed_out;
+  if (t == 0) timed_out = 0;
+  __syncthreads();
   if (t < size) {
     const long long t0 = wall_clock64();
     while (__hip_atomic_load(xflags(me) + slot * kXMaxRanks + t, __ATOMIC_ACQUIRE,
                              __HIP_MEMORY_SCOPE_SYSTEM) != seq) {
       if (wall_clock64() - t0 > timeout_ticks) {
         atomicExch(err, 1);
+        timed_out = 1;
         break;
       }
       __builtin_amdgcn_s_sleep(2);
@@ -61,7 +68,7 @@ __device__ __forceinline__ void xgmi_block_allreduce(const XgmiPeers& peers, int
     for (int q = 0; q < size; ++q)
       s += __hip_atomic_load(xdata(me) + (slot * kXMaxRanks + q) * kXMaxFloats + t,
                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    vals[t] = s;
+    vals[t] = timed_out ? __builtin_nanf("") : s;
   }
   __syncthreads();
   if (t == 0) *seq_ptr = seq;

@@ -74,6 +74,13 @@ int64_t xgmi_open(pybind11::bytes handle) {
   return reinterpret_cast<int64_t>(p);
 }
 
+// Re-zero this rank's region (flags and inboxes); the caller has drained every kernel
+// and synchronised with the peers before and after (OneShotAllReduce.reset).
+void xgmi_zero(int64_t base) {
+  xcheck(hipMemset(reinterpret_cast<void*>(base), 0, kXRegionBytes), "hipMemset");
+  xcheck(hipDeviceSynchronize(), "hipDeviceSynchronize");
+}
+
 void xgmi_close(int64_t ptr) { (void)hipIpcCloseMemHandle(reinterpret_cast<void*>(ptr)); }
 void xgmi_free(int64_t ptr) { (void)hipFree(reinterpret_cast<void*>(ptr)); }
 

@@ -571,6 +571,7 @@ class FusedAdamEngine:
     def trajectory(self) -> torch.Tensor:
         """The recorded parameter trajectory (assembled across ranks under ZeRO)."""
         self.drain()
+        self.check("trajectory", collective=True)
         if self.traj_loc is None:
             return self.to_user(self.history.result())
         if self.owner:
@@ -592,13 +593,43 @@ class FusedAdamEngine:
 
     def params(self) -> torch.Tensor:
         self.drain()
+        self.check("params", collective=True)
         if self.owner:
             a, b = self.own_range
             return self.to_user(self._assemble(self.theta[a:b]))
         return self.to_user(self.theta[:self.P])
 
     def last_loss(self) -> float:
-        return float(self.loss.item())
+        loss = float(self.loss.item())
+        self.check("last_loss")
+        return loss
+
+    def check(self, where: str = "", collective: bool = False) -> None:
+        """Raise :class:`~multigrad_amd.parallel.xgmi.CollectiveTimeout` if a peer-memory
+        exchange of this engine timed out (its results are NaN-poisoned); a host sync.
+
+        ``collective=True`` all-reduces the verdict so every rank raises together (used
+        where the caller goes on to a collective: ``params``, ``trajectory``,
+        checkpoints, the periodic check of :meth:`run_adam`); ``last_loss`` and
+        ``state_dict`` check locally."""
+        if self.oneshot is not None:
+            self.oneshot.check(where or f"engine step {self.step_host}",
+                               comm=self.comm if collective else None)
+
+    def grad_collective_name(self) -> str:
+        """Human-readable name of the per-step gradient collective (bench records)."""
+        if self.size == 1:
+            return "none (1 rank)"
+        if self.owner:
+            return "none: owner-local gradients, sumstat all-reduce only"
+        if self.zero:
+            return "RCCL reduce-scatter + all-gather (ZeRO-1)"
+        return "RCCL all-reduce"
+
+    def sumstat_collective_name(self) -> str:
+        if self.size == 1:
+            return "none (1 rank)"
+        return "xGMI one-shot kernel (self-tested)" if self.oneshot is not None else "RCCL"
 
     # ------------------------------------------------------------------ L-BFGS objective
     def lbfgs_objective(self, guess):
@@ -624,6 +655,7 @@ class FusedAdamEngine:
         """This rank's optimizer state after ``step_host`` steps: owned slices under ZeRO
         and owner mode (one file per rank), everything otherwise."""
         self.drain()
+        self.check("state_dict")  # never checkpoint NaN-poisoned state
         mode = "owner" if self.owner else "zero" if self.zero else "replicated"
         u = self.u_loc if self.sharded else (self.u if self.bounds is not None else None)
         st = {"mode": mode, "size": self.size, "rank": self.rank, "P": self.P,
@@ -650,6 +682,8 @@ class FusedAdamEngine:
                              f"this engine ({mode}, {self.size} ranks)")
         dev = self.device
         step = int(st["step"])
+        from ..utils.checkpoint import check_loaded_step
+        check_loaded_step(step, self.comm if self.size > 1 else None)
         self.m.copy_(st["m"].to(dev))
         self.v.copy_(st["v"].to(dev))
         th = st["theta"].to(dev)
@@ -685,6 +719,8 @@ class FusedAdamEngine:
 
     def save_checkpoint(self, path: str) -> None:
         from ..utils import checkpoint as ckpt
+        self.drain()
+        self.check("checkpoint", collective=True)
         ckpt.save_optimizer_state(path, self.state_dict(), comm=self.comm if self.size > 1 else None,
                                   sharded=self.sharded)
 
@@ -709,13 +745,19 @@ class FusedAdamEngine:
         self.setup(guess, nsteps, param_bounds, learning_rate, b1, b2, eps, history,
                    legacy_bounds_jacobian)
         start = self.load_checkpoint(resume_from) if resume_from is not None else 0
-        for i in range(start, int(nsteps)):
-            self.step()
-            if callback is not None:
-                callback(i, self.loss, self)
-            if checkpoint_path and checkpoint_every and (i + 1) % checkpoint_every == 0:
-                self.save_checkpoint(checkpoint_path)
-        return self.trajectory()
+        from ..utils.hooks import StepHooks, driver_guard
+        hooks = StepHooks(self.comm, callback)  # MULTIGRAD_CHECK_EVERY / MULTIGRAD_METRICS
+        err_every = int(os.environ.get("MULTIGRAD_ERR_CHECK_EVERY", "100") or 0)
+        with driver_guard(self.comm):
+            for i in range(start, int(nsteps)):
+                self.step()
+                if hooks.active:
+                    hooks(i, self.loss, self, self.params)
+                if err_every and self.oneshot is not None and (i + 1) % err_every == 0:
+                    self.check(collective=True)
+                if checkpoint_path and checkpoint_every and (i + 1) % checkpoint_every == 0:
+                    self.save_checkpoint(checkpoint_path)
+            return self.trajectory()
 
 
 class _EngineObjective:
@@ -766,7 +808,9 @@ class _EngineObjective:
 
     def __call__(self, x: torch.Tensor):
         loss, g = self.device_call(x)
-        return float(loss.double().item()), g
+        f = float(loss.double().item())
+        self.e.check("L-BFGS evaluation")
+        return f, g
 
     def device_call(self, x: torch.Tensor):
         """``(loss, grad)`` with the loss left on the device (1-element tensor), so the

@@ -22,6 +22,7 @@ import torch
 
 from .parallel.comm import get_world_comm
 from .parallel.subcomm import distribute_data as _distribute_data
+from .utils.hooks import StepHooks, driver_guard
 from .utils.tensors import as_param_tensor
 
 __all__ = ["distribute_data", "reduce_sum", "simple_grad_descent"]
@@ -96,8 +97,12 @@ def simple_grad_descent(data_dict, loss_and_grad_func: Callable, guess, learning
             params.copy_(saved)
             step.zero_()
     if not done:
-        for _ in range(n):
-            body()
+        hooks = StepHooks(comm)  # MULTIGRAD_CHECK_EVERY / MULTIGRAD_METRICS (eager steps)
+        with driver_guard(comm):
+            for i in range(n):
+                body()
+                if hooks.active:
+                    hooks(i, losses[i], None, lambda: params)
     loss_np = losses.detach().cpu().numpy()
     par_np = hist.detach().cpu().numpy()
     return pd.DataFrame(dict(loss=list(loss_np), params=list(par_np)))

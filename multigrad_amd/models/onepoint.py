@@ -58,7 +58,8 @@ class _OptimizerFrontEnds:
         return util.simple_grad_descent(
             None, guess=as_param_tensor(guess, device=self.param_device()), nsteps=nsteps,
             learning_rate=learning_rate,
-            loss_and_grad_func=self.calc_loss_and_grad_from_params, has_aux=has_aux)
+            loss_and_grad_func=self.calc_loss_and_grad_from_params, has_aux=has_aux,
+            comm=self._opt_comm())
 
     def run_adam(self, guess, nsteps: int = 100, param_bounds=None, learning_rate: float = 0.01,
                  randkey=None, const_randkey: bool = False, comm=None, **kw):

@@ -26,6 +26,7 @@ from typing import Any, Callable, Optional
 
 import torch
 
+from ..utils.hooks import StepHooks, driver_guard
 from ..utils.progress import trange
 from ..utils.random import PRNGKey, gen_new_key, init_randkey
 from ..utils.tensors import as_param_tensor
@@ -216,21 +217,23 @@ def run_adam(logloss_and_grad_fn: Callable, params, data, nsteps: int = 100,
         n = min(prev.shape[0], hist.buf.shape[0])
         hist.buf[:n].copy_(prev[:n])
     kwargs: dict = {}
-    for step in trange(nsteps, desc="Adam Gradient Descent Progress"):
-        if step < start:
-            continue
-        if key is not None:
-            key, key_i = key.split(2)
-            kwargs["randkey"] = key_i
-        loss, grad = logloss_and_grad_fn(opt.params(), data, **kwargs)
-        row = hist.row_for(step)
-        opt.update(torch.as_tensor(grad), traj_row=None if row is None else row.reshape(-1))
-        hist.record(step, opt.params())
-        if callback is not None:
-            callback(step, loss, opt)
-        if checkpoint_path and checkpoint_every and (step + 1) % checkpoint_every == 0:
-            ckpt.save_optimizer_state(checkpoint_path, {
-                "adam": opt.state_dict(), "randkey": None if key is None else key.value,
-                "history": hist.buf[:step + 2].cpu() if history == "full" else None},
-                comm=comm)
+    hooks = StepHooks(comm, callback)  # MULTIGRAD_CHECK_EVERY / MULTIGRAD_METRICS
+    with driver_guard(comm):
+        for step in trange(nsteps, desc="Adam Gradient Descent Progress"):
+            if step < start:
+                continue
+            if key is not None:
+                key, key_i = key.split(2)
+                kwargs["randkey"] = key_i
+            loss, grad = logloss_and_grad_fn(opt.params(), data, **kwargs)
+            row = hist.row_for(step)
+            opt.update(torch.as_tensor(grad), traj_row=None if row is None else row.reshape(-1))
+            hist.record(step, opt.params())
+            if hooks.active:
+                hooks(step, loss, opt, opt.params)
+            if checkpoint_path and checkpoint_every and (step + 1) % checkpoint_every == 0:
+                ckpt.save_optimizer_state(checkpoint_path, {
+                    "adam": opt.state_dict(), "randkey": None if key is None else key.value,
+                    "history": hist.buf[:step + 2].cpu() if history == "full" else None},
+                    comm=comm)
     return hist.result()

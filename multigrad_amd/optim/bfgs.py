@@ -18,6 +18,7 @@ import numpy as np
 import scipy.optimize
 import torch
 
+from ..utils.hooks import StepHooks
 from ..utils.progress import progress_enabled
 from ..utils.random import init_randkey
 from ..utils.tensors import as_param_tensor
@@ -83,9 +84,16 @@ def run_bfgs(loss_and_grad_fn: Callable, params, maxsteps: int = 100, param_boun
                 comm.broadcast(cmd, root=0)
             return evaluate(x)
 
-        def callback(*_a, **_k):
+        hooks = StepHooks(None)  # metrics only: the workers are inside the command loop
+        nit = [0]
+
+        def callback(*a, **_k):
             if pbar is not None:
                 pbar.update()
+            if hooks.active:
+                res = _k.get("intermediate_result")
+                hooks(nit[0], None if res is None else float(res.fun), None)
+            nit[0] += 1
 
         result = scipy.optimize.minimize(fun, x0=x0, method="L-BFGS-B", jac=True,
                                          options=dict(maxiter=maxsteps, **(options or {})),

@@ -131,6 +131,8 @@ def lbfgs_minimize(obj, maxiter: int = 100, m: int = 10, ftol: float = 1e7 * _EP
 
     status, message = 1, "STOP: TOTAL NO. of ITERATIONS REACHED LIMIT"
     nit = 0
+    from ..utils.hooks import StepHooks
+    hooks = StepHooks(comm, what="L-BFGS iterate")  # MULTIGRAD_CHECK_EVERY / _METRICS
     if ginf(g) <= gtol:
         status, message = 0, "CONVERGENCE: NORM_OF_PROJECTED_GRADIENT_<=_PGTOL"
     else:
@@ -231,6 +233,8 @@ def lbfgs_minimize(obj, maxiter: int = 100, m: int = 10, ftol: float = 1e7 * _EP
             f_old, f, g = f, f_new, g_new
             if callback is not None:
                 callback(obj.full(x))
+            if hooks.active:
+                hooks(k, f, None, (lambda: x) if not sharded else None)
             if ginf(g) <= gtol:
                 status, message = 0, "CONVERGENCE: NORM_OF_PROJECTED_GRADIENT_<=_PGTOL"
                 break

@@ -343,7 +343,7 @@ class TorchComm(Comm):
     def all_reduce(self, tensor, op=SUM, async_op=False):
         c10d = _c10d()
         if tensor.is_cuda:
-            from .xgmi import maybe_oneshot  # MULTIGRAD_ALLREDUCE=oneshot (opt-in)
+            from .xgmi import maybe_oneshot  # only with MULTIGRAD_ALLREDUCE=oneshot (opt-in)
             if maybe_oneshot(self, tensor, op) is not None:
                 return _DoneWork() if async_op else None
         if not tensor.is_contiguous():
@@ -571,6 +571,11 @@ def init_distributed(backend: Optional[str] = None, timeout: Optional[float] = N
 
 
 def _wrap_default_group() -> Comm:
+    from ..utils.debug import maybe_fingerprint  # MULTIGRAD_FINGERPRINT=1
+    return maybe_fingerprint(_default_group_comm())
+
+
+def _default_group_comm() -> Comm:
     import torch.distributed as dist
     from torch.distributed import distributed_c10d as c10
     pg = c10._get_default_group()
@@ -603,7 +608,8 @@ def get_world_comm() -> Comm:
         elif launcher_env()["size"] > 1:
             _WORLD = init_distributed()
         else:
-            _WORLD = SerialComm()
+            from ..utils.debug import maybe_fingerprint
+            _WORLD = maybe_fingerprint(SerialComm())
     return _WORLD
 
 

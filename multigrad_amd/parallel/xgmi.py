@@ -9,8 +9,19 @@ It replaces RCCL for tiny device all-reduces (K <= 64 fp32, SUM: the engine's pe
 sumstats) on up to 8 ranks.  The context is built on the first eligible call and checked
 by a self-test on the actual hardware; only if every rank passes it is it used --
 otherwise (or with ``MULTIGRAD_ALLREDUCE=rccl``, or without IPC, e.g. ranks on several
-nodes) RCCL is.  Validated with two processes sharing one GPU (tests/test_xgmi_gpu.py,
-3.8 us per call there); the cross-GPU path is covered by the start-up self-test.
+nodes, or without the native extension) RCCL is.
+
+``MULTIGRAD_ALLREDUCE``:
+  ``auto`` (default) -- the fused engine's per-step sumstat exchange uses it;
+      ``Comm.all_reduce`` of user code stays on RCCL.
+  ``oneshot`` -- additionally every eligible ``Comm.all_reduce`` (checked after each call).
+  ``rccl`` -- never.
+
+Failure is loud: a peer that does not signal within ``MULTIGRAD_ONESHOT_TIMEOUT`` seconds
+sets the device error word and poisons the result with NaN (``csrc/xgmi.h``); the engine
+reads the word at its host sync points (``FusedAdamEngine.check``) and raises
+:class:`CollectiveTimeout` naming the rank and sequence number.  :meth:`reset`
+(collective) re-zeroes the protocol state so a caller can continue after handling it.
 
 Reference counterpart: the per-evaluation ``MPI.Allreduce`` of the sumstats,
 multigrad/multigrad.py:522.
@@ -22,17 +33,29 @@ from typing import Optional
 
 import torch
 
-from ..ops._ext import ext
-
-__all__ = ["OneShotAllReduce", "oneshot_enabled", "connect", "get_oneshot", "MAX_FLOATS",
-           "MAX_RANKS"]
+__all__ = ["OneShotAllReduce", "CollectiveTimeout", "oneshot_enabled", "oneshot_mode",
+           "connect", "get_oneshot", "maybe_oneshot", "MAX_FLOATS", "MAX_RANKS"]
 
 MAX_FLOATS = 64
 MAX_RANKS = 8
 
 
+class CollectiveTimeout(RuntimeError):
+    """A peer-memory collective timed out waiting for a peer: its result is invalid."""
+
+
+def oneshot_mode() -> str:
+    m = os.environ.get("MULTIGRAD_ALLREDUCE", "auto").lower()
+    return m if m in ("auto", "oneshot", "rccl") else "auto"
+
+
 def oneshot_enabled() -> bool:
-    return os.environ.get("MULTIGRAD_ALLREDUCE", "auto").lower() in ("auto", "oneshot")
+    """Whether the engine's sumstat exchange may use the one-shot kernel."""
+    return oneshot_mode() in ("auto", "oneshot")
+
+
+def _timeout_s() -> float:
+    return float(os.environ.get("MULTIGRAD_ONESHOT_TIMEOUT", "5"))
 
 
 class OneShotAllReduce:
@@ -55,12 +78,45 @@ class OneShotAllReduce:
                      or getattr(op, "name", "") == "SUM"))
 
     def __call__(self, t: torch.Tensor) -> torch.Tensor:
+        from ..ops._ext import ext
         ext().xgmi_allreduce(t, self.peers, self.rank, self.seq, self.err, self.timeout_s)
         return t
 
     def ok(self) -> bool:
         """False if any call timed out waiting for a peer (host sync)."""
         return int(self.err.item()) == 0
+
+    def check(self, where: str = "", comm=None) -> None:
+        """Raise :class:`CollectiveTimeout` if any exchange so far timed out (host sync).
+
+        With ``comm`` the verdict is all-reduced first (collective: every rank raises
+        together, so no rank is left waiting in a later collective)."""
+        e, s = (int(x) for x in torch.cat([self.err, self.seq]).tolist())
+        bad = [self.rank] if e else []
+        if comm is not None and comm.size > 1:
+            flags = torch.zeros(comm.size, dtype=torch.int64)
+            flags[comm.rank] = 1 if e else 0
+            comm.all_reduce(flags)
+            bad = [r for r in range(comm.size) if int(flags[r])]
+        if bad:
+            raise CollectiveTimeout(
+                f"rank {self.rank}/{self.size}: one-shot xGMI exchange timed out after "
+                f"{self.timeout_s:g} s waiting for a peer on rank(s) {bad} (sequence {s}"
+                f"{', ' + where if where else ''}); its sums are NaN-poisoned.  A rank "
+                f"skipped a collective or fell behind by more than MULTIGRAD_ONESHOT_TIMEOUT; "
+                f"call reset() on every rank (collective) before reusing the communicator")
+
+    def reset(self, comm) -> None:
+        """Collective: return the protocol to its initial state on every rank (after a
+        timeout was handled).  Every rank's kernels are drained first."""
+        from ..ops._ext import ext
+        torch.cuda.synchronize()
+        comm.barrier()
+        ext().xgmi_zero(self.base)
+        self.seq.zero_()
+        self.err.zero_()
+        torch.cuda.synchronize()
+        comm.barrier()
 
     def self_test(self) -> bool:
         """A few calls with rank-dependent values whose sums are exact in fp32; True when
@@ -77,6 +133,7 @@ class OneShotAllReduce:
         return self.ok()
 
     def close(self) -> None:
+        from ..ops._ext import ext
         E = ext()
         for r, p in enumerate(self.peers):
             if r != self.rank and p:
@@ -89,13 +146,16 @@ class OneShotAllReduce:
 def connect(comm, timeout_s: float = 5.0, test: bool = True) -> Optional[OneShotAllReduce]:
     """Collective: export, exchange and map the regions of every rank of ``comm``, then
     self-test.  Each phase ends with an all-gather of the per-rank verdicts, so all ranks
-    take the same branch; returns None (use RCCL) if any rank failed any phase."""
-    E = ext()
+    take the same branch; returns None (use RCCL) if any rank failed any phase -- a
+    missing native extension included."""
+    E = None
     base, handle = 0, None
     try:
+        from ..ops._ext import ext
+        E = ext()
         base = E.xgmi_alloc()
         handle = bytes(E.xgmi_handle(base))
-    except Exception as exc:  # noqa: BLE001
+    except Exception as exc:  # noqa: BLE001  (no extension / no IPC on this rank)
         _debug(exc)
     handles = comm.allgather(handle)
     peers, ok = [], all(h is not None for h in handles)
@@ -105,10 +165,15 @@ def connect(comm, timeout_s: float = 5.0, test: bool = True) -> Optional[OneShot
         except Exception as exc:  # noqa: BLE001  (no IPC between these ranks)
             ok = False
             _debug(exc)
-    ar = OneShotAllReduce(comm.rank, comm.size, base, peers, timeout_s)
     if not all(comm.allgather(ok)):
-        ar.close()
+        if E is not None:
+            for r, p in enumerate(peers):
+                if r != comm.rank and p:
+                    E.xgmi_close(p)
+            if base:
+                E.xgmi_free(base)
         return None
+    ar = OneShotAllReduce(comm.rank, comm.size, base, peers, timeout_s)
     comm.barrier()  # every region is zeroed and mapped before any rank writes into it
     ok = ar.self_test() if test else True
     if not all(comm.allgather(bool(ok))):
@@ -124,32 +189,31 @@ def _debug(exc) -> None:
 
 
 def maybe_oneshot(comm, t: torch.Tensor, op) -> Optional[torch.Tensor]:
-    """Run ``t`` through the communicator's one-shot all-reduce when enabled and
-    applicable; None otherwise (the caller uses RCCL).
-
-    ``MULTIGRAD_ALLREDUCE``: ``rccl`` never; ``auto`` (default) / ``oneshot`` connect on
-    the first eligible call (collective) and use it only if every rank passed the
-    self-test."""
-    if not oneshot_enabled() or comm.size > MAX_RANKS or not OneShotAllReduce.supports(t, op):
+    """``Comm.all_reduce`` hook: run ``t`` through the communicator's one-shot all-reduce
+    when ``MULTIGRAD_ALLREDUCE=oneshot`` (opt-in for user code) and applicable; None
+    otherwise (the caller uses RCCL).  Each call is checked (host sync) so a timed-out
+    exchange raises here instead of returning a wrong sum."""
+    if oneshot_mode() != "oneshot" or comm.size > MAX_RANKS or not OneShotAllReduce.supports(t, op):
         return None
     ar = getattr(comm, "_oneshot", None)
     if ar is None:
-        ar = comm._oneshot = connect(
-            comm, float(os.environ.get("MULTIGRAD_ONESHOT_TIMEOUT", "5"))) or False
+        ar = comm._oneshot = connect(comm, _timeout_s()) or False
     if ar is False:
         return None
-    return ar(t)
+    ar(t)
+    ar.check("Comm.all_reduce")
+    return t
 
 
 def get_oneshot(comm) -> Optional[OneShotAllReduce]:
-    """The communicator's one-shot context, connecting it now if needed (collective: call
-    on every rank); None when disabled or unavailable (use RCCL)."""
+    """The communicator's one-shot context for the fused engine, connecting it now if
+    needed (collective: call on every rank); None when disabled or unavailable (use
+    RCCL)."""
     if comm is None or comm.size == 1 or not oneshot_enabled() or comm.size > MAX_RANKS:
         return None
     if not torch.cuda.is_available():
         return None
     ar = getattr(comm, "_oneshot", None)
     if ar is None:
-        ar = comm._oneshot = connect(
-            comm, float(os.environ.get("MULTIGRAD_ONESHOT_TIMEOUT", "5"))) or False
+        ar = comm._oneshot = connect(comm, _timeout_s()) or False
     return ar or None

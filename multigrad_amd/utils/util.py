@@ -13,6 +13,7 @@ import torch
 from scipy.stats import qmc
 
 from ..parallel.subcomm import scatter_nd
+from .hooks import StepHooks, driver_guard
 from .progress import trange
 from .tensors import as_param_tensor
 
@@ -55,13 +56,16 @@ def value_and_grad(loss_func, has_aux: bool = False, **call_kwargs):
 
 
 def simple_grad_descent(loss_func, guess, nsteps, learning_rate, loss_and_grad_func=None,
-                        grad_loss_func=None, has_aux=False, **kwargs) -> GradDescentResult:
+                        grad_loss_func=None, has_aux=False, *, comm=None, callback=None,
+                        **kwargs) -> GradDescentResult:
     """Fixed-learning-rate gradient descent (reference ``multigrad/util.py:80-134``).
 
     SPMD: every rank runs the same loop with identical all-reduced gradients, so no
     broadcast is needed.  The recorded ``params[i]`` are the parameters at which
     ``loss[i]`` was evaluated (the final update is not recorded), exactly as in the
     reference.  Losses and parameters stay on the parameters' device until the end.
+    ``comm`` (the communicator the gradient is reduced over) and ``callback(step, loss,
+    None)`` feed the per-step driver hooks (:mod:`multigrad_amd.utils.hooks`).
     """
     if loss_and_grad_func is None:
         if grad_loss_func is None:
@@ -72,15 +76,19 @@ def simple_grad_descent(loss_func, guess, nsteps, learning_rate, loss_and_grad_f
 
     params = as_param_tensor(guess)
     losses, plist, auxes = [], [], []
-    for _ in trange(nsteps, desc="Simple Gradient Descent Progress"):
-        (loss, grad), aux = loss_and_grad_func(params), None
-        if has_aux:
-            (loss, aux), grad = loss, grad
-        losses.append(torch.as_tensor(loss).detach())
-        plist.append(params)
-        auxes.append(aux)
-        params = params - learning_rate * torch.as_tensor(grad, device=params.device,
-                                                          dtype=params.dtype)
+    hooks = StepHooks(comm, callback)  # MULTIGRAD_CHECK_EVERY / MULTIGRAD_METRICS
+    with driver_guard(comm):
+        for step in trange(nsteps, desc="Simple Gradient Descent Progress"):
+            (loss, grad), aux = loss_and_grad_func(params), None
+            if has_aux:
+                (loss, aux), grad = loss, grad
+            losses.append(torch.as_tensor(loss).detach())
+            plist.append(params)
+            auxes.append(aux)
+            params = params - learning_rate * torch.as_tensor(grad, device=params.device,
+                                                              dtype=params.dtype)
+            if hooks.active:
+                hooks(step, loss, None, lambda: params)
     loss_t = torch.stack(losses) if losses else torch.zeros(0)
     params_t = torch.stack(plist) if plist else torch.zeros((0,) + tuple(params.shape))
     aux_out: Any = auxes

@@ -1,0 +1,162 @@
+"""The aux subsystems wired into the drivers: each environment
+knob is set and its effect observed -- MULTIGRAD_CHECK_EVERY (bitwise rank agreement of
+the parameters), MULTIGRAD_METRICS (JSONL per step from every driver),
+MULTIGRAD_FINGERPRINT (collective signature cross-check), the sharded checkpoint commit
+manifest, the 2-"node" split_subcomms_by_node, and bench.py's self-launch of N ranks."""
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+import multigrad_amd as mg
+from multigrad_amd.parallel import comm as C
+from multigrad_amd.utils import checkpoint as ckpt
+from multigrad_amd.utils import debug
+
+from distributed import run_distributed
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+# ------------------------------------------------------------------ MULTIGRAD_CHECK_EVERY
+def _check_every_body(rank, size, diverge):
+    os.environ["MULTIGRAD_CHECK_EVERY"] = "2"
+    from multigrad_amd.optim.adam import run_adam
+    comm = mg.get_world_comm()
+    target = torch.tensor([1.0, -2.0, 0.5])
+
+    def lg(p, _):
+        g = 2 * (p - target)
+        if diverge and rank == 1:
+            g = g * 1.5  # a rank whose gradient was never summed: parameters drift apart
+        return ((p - target) ** 2).sum(), g
+
+    try:
+        run_adam(lg, torch.zeros(3), None, nsteps=6, learning_rate=0.1, comm=comm)
+        return "ok"
+    except debug.CollectiveMismatch as e:
+        return "mismatch: " + str(e)[:40]
+
+
+def test_check_every_detects_rank_divergence():
+    ok = run_distributed(_check_every_body, 2, False)
+    assert ok == ["ok", "ok"]
+    bad = run_distributed(_check_every_body, 2, True)
+    assert all(r.startswith("mismatch") and "after step 1" in r for r in bad), bad
+
+
+# ------------------------------------------------------------------ MULTIGRAD_METRICS
+def test_metrics_env_installs_logger_in_every_driver(tmp_path, monkeypatch):
+    from multigrad_amd.models.toy import SumOfSquaresModel, make_toy_data
+    from multigrad_amd.models.population import PopulationSMFModel, make_population_data
+    C.set_world_comm(None)
+    path = tmp_path / "metrics.jsonl"
+    monkeypatch.setenv("MULTIGRAD_METRICS", str(path))
+    m = SumOfSquaresModel(aux_data=make_toy_data(ndim=3, npoints=20))
+    m.run_adam(torch.zeros(3), nsteps=3, learning_rate=0.1)
+    m.run_simple_grad_descent(torch.zeros(3), nsteps=2, learning_rate=0.01)
+    m.run_bfgs(torch.zeros(3), maxsteps=3, method="device")
+    n_generic = len(path.read_text().splitlines())
+    data = make_population_data(400, 4000, seed=3, device=torch.device("cpu"))
+    pm = PopulationSMFModel(aux_data=data)
+    pm.set_target_from_truth()
+    pm.run_adam(data["guess"], nsteps=2, learning_rate=1e-3)
+    recs = [json.loads(line) for line in path.read_text().splitlines()]
+    assert n_generic >= 3 + 2 + 1
+    assert len(recs) == n_generic + 2
+    assert all("step" in r and "loss" in r and "step_time_s" in r for r in recs)
+    assert [r["step"] for r in recs[:3]] == [0, 1, 2]
+
+
+# ------------------------------------------------------------------ MULTIGRAD_FINGERPRINT
+def _fingerprint_body(rank, size):
+    os.environ["MULTIGRAD_FINGERPRINT"] = "1"
+    C.set_world_comm(C._wrap_default_group())
+    comm = mg.get_world_comm()
+    wrapped = isinstance(comm, debug.CollectiveFingerprint)
+    t = torch.ones(2)
+    comm.all_reduce(t)
+    sub = comm.split(0)
+    sub_wrapped = isinstance(sub, debug.CollectiveFingerprint)
+    try:
+        comm.all_reduce(torch.ones(2 + rank))
+        caught = False
+    except debug.CollectiveMismatch:
+        caught = True
+    return wrapped, sub_wrapped, float(t[0]), caught
+
+
+def test_fingerprint_env_wraps_world():
+    res = run_distributed(_fingerprint_body, 2)
+    assert all(r == (True, True, 2.0, True) for r in res), res
+
+
+# ------------------------------------------------------------------ checkpoint commit
+def _ckpt_body(rank, size, path):
+    comm = mg.get_world_comm()
+    ckpt.save_optimizer_state(path, {"step": 5, "size": size, "x": torch.ones(2) * rank},
+                              comm=comm, sharded=True)
+    st = ckpt.load_optimizer_state(path, rank=rank, sharded=True)
+    ckpt.check_loaded_step(st["step"], comm)
+    # an interrupted later checkpoint: rank 1's shard moves to step 9, the manifest does not
+    comm.barrier()
+    if rank == 1:
+        torch.save({"step": 9, "size": size}, ckpt.shard_path(path, 1))
+    comm.barrier()
+    try:
+        ckpt.load_optimizer_state(path, rank=rank, sharded=True)
+        torn = False
+    except ckpt.CheckpointMismatch:
+        torn = True
+    try:
+        ckpt.check_loaded_step(5 + rank, comm)
+        skew = False
+    except ckpt.CheckpointMismatch:
+        skew = True
+    return float(st["x"][0]), torn, skew
+
+
+def test_sharded_checkpoint_manifest(tmp_path):
+    res = run_distributed(_ckpt_body, 2, str(tmp_path / "opt.pt"))
+    assert res[0] == (0.0, False, True) and res[1] == (1.0, True, True)
+    man = json.loads(open(ckpt.manifest_path(str(tmp_path / "opt.pt"))).read())
+    assert man == {"step": 5, "size": 2, "sharded": True}
+
+
+# ------------------------------------------------------------------ two "nodes"
+def _nodes_body(rank, size):
+    os.environ["MULTIGRAD_NODE_NAME"] = "nodeB" if rank % 2 else "nodeA"
+    sub, nnodes, node = mg.split_subcomms_by_node()
+    t = torch.tensor([float(rank)])
+    sub.all_reduce(t)
+    return nnodes, node, sub.size, sub.rank, float(t[0]), sub.name
+
+
+def test_split_subcomms_by_node_two_nodes():
+    res = run_distributed(_nodes_body, 4)
+    assert [r[:4] for r in res] == [(2, 0, 2, 0), (2, 1, 2, 0), (2, 0, 2, 1), (2, 1, 2, 1)]
+    assert [r[4] for r in res] == [2.0, 4.0, 2.0, 4.0]  # ranks {0,2} on A, {1,3} on B
+
+
+# ------------------------------------------------------------------ bench self-launch
+def test_bench_self_launches_n_ranks():
+    env = dict(os.environ, MULTIGRAD_PROGRESS="0", OMP_NUM_THREADS="1",
+               MULTIGRAD_DEVICE_COMM="0", HIP_VISIBLE_DEVICES="", CUDA_VISIBLE_DEVICES="")
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--params", "2000",
+                        "--halos", "20000", "--steps", "3", "--warmup", "1"], cwd=ROOT, env=env,
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    rec = lines[0]
+    assert rec["n_gpus"] == 2 and rec["value"] > 0
+    assert rec["config"]["placement"] == "hashed"
+    assert rec["config"]["optimizer_sharding"] == "zero1"
+    assert rec["owner_steps_per_s"] > 0
+    assert rec["owner_config"]["optimizer_sharding"] == "owner"

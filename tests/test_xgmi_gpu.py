@@ -79,3 +79,80 @@ def test_engine_with_oneshot_sumstat_allreduce():
     assert not ref[0][1] and res[0][1] and res[1][1]
     np.testing.assert_array_equal(res[0][0], res[1][0])
     np.testing.assert_allclose(res[0][0], ref[0][0], rtol=1e-5, atol=1e-6)
+
+
+def _late_peer(rank, size):
+    """Rank 1 reaches the exchange 1.5 s after rank 0 (timeout 0.3 s): rank 0's result
+    must be NaN-poisoned and check() must raise -- never a silently partial sum; after a
+    collective reset() the protocol works again."""
+    import time
+    import multigrad_amd as mg
+    from multigrad_amd.parallel.xgmi import CollectiveTimeout, connect
+    comm = mg.get_world_comm()
+    dev = torch.device("cuda", 0)
+    ar = connect(comm, timeout_s=0.3)
+    assert ar is not None
+    comm.barrier()
+    if rank == 1:
+        time.sleep(1.5)
+    t = torch.full((8,), float(rank + 1), device=dev)
+    ar(t)
+    torch.cuda.synchronize()
+    vals = t.cpu().numpy()
+    try:
+        ar.check("test")
+        raised = ""
+    except CollectiveTimeout as e:
+        raised = str(e)
+    ar.reset(comm)
+    t2 = torch.full((4,), float(rank + 1), device=dev)
+    ar(t2)
+    after = t2.cpu().numpy()
+    ok_after = ar.ok()
+    ar.close()
+    return vals, raised, after, ok_after
+
+
+def test_oneshot_late_peer_fails_loudly():
+    (v0, e0, a0, ok0), (v1, e1, a1, ok1) = run_distributed(_late_peer, 2, timeout=300)
+    assert np.isnan(v0).all() and "timed out" in e0 and "rank 0/2" in e0
+    np.testing.assert_array_equal(v1, np.full(8, 3.0, dtype=np.float32))  # the late rank
+    assert e1 == ""                                                      # saw both values
+    np.testing.assert_array_equal(a0, np.full(4, 3.0, dtype=np.float32))
+    np.testing.assert_array_equal(a1, a0)
+    assert ok0 and ok1
+
+
+def _engine_err(rank, size):
+    import multigrad_amd as mg
+    from multigrad_amd.engine.fused import FusedAdamEngine
+    from multigrad_amd.models.population import PopulationSMFModel, make_population_data
+    from multigrad_amd.parallel.xgmi import CollectiveTimeout
+    comm = mg.get_world_comm()
+    dev = torch.device("cuda", 0)
+    data = make_population_data(4000, 200_000, seed=5, comm=comm, device=dev, placement="owner")
+    model = PopulationSMFModel(aux_data=data, comm=comm)
+    model.set_target_from_truth()
+    eng = FusedAdamEngine(model)
+    eng.setup(data["guess"], nsteps=4, learning_rate=1e-3)
+    assert eng.oneshot is not None
+    eng.step()
+    eng.step()
+    eng.params()  # clean so far
+    if rank == 0:
+        eng.oneshot.err.fill_(1)  # as a timed-out exchange leaves it
+    out = []
+    # local checks (last_loss, state_dict) raise on the failed rank only; the collective
+    # ones (params, trajectory: they all-gather afterwards) raise on every rank together
+    for fn in (eng.last_loss, eng.state_dict, eng.params, eng.trajectory):
+        try:
+            fn()
+            out.append(False)
+        except CollectiveTimeout:
+            out.append(True)
+    return out
+
+
+def test_engine_raises_on_exchange_error():
+    r0, r1 = run_distributed(_engine_err, 2, timeout=300)
+    assert r0 == [True, True, True, True] and r1 == [False, False, True, True]
