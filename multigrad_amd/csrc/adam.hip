@@ -15,6 +15,7 @@
 // (eager callers may pass the step instead: no counter traffic at all).
 // Memory: 16 B read + 12 B written per unbounded parameter (+8 B read, +4 B written for
 // the bounded p output, +4 B for the trajectory) -> HBM-bandwidth bound; float4 lanes.
+#include "adam.h"
 #include "common.h"
 
 #include <torch/extension.h>
@@ -23,9 +24,6 @@
 namespace mg {
 
 constexpr int kAdamThreads = 256;
-constexpr float kPi = 3.14159265358979323846f;
-
-enum BoundKind : int8_t { kNone = 0, kBoth = 1, kLow = 2, kHigh = 3 };
 
 struct AdamArgs {
   float* u;
@@ -43,43 +41,6 @@ struct AdamArgs {
   int host_step;       // >= 0: the 0-based step, passed by an eager caller; -1: read *step
   float lr, b1, b2, eps;
 };
-
-__device__ __forceinline__ float dpdu(float at, float lo, float hi, int8_t k) {
-  if (k == kBoth) {
-    const float s = (hi - lo) / kPi;
-    const float r = at / s;
-    return 1.0f / (1.0f + r * r);
-  }
-  if (k == kLow || k == kHigh) {
-    const float q = at / sqrtf(at * at + 4.0f);
-    return 0.5f * (k == kLow ? 1.0f + q : 1.0f - q);
-  }
-  return 1.0f;
-}
-
-__device__ __forceinline__ float inv_transform(float u, float lo, float hi, int8_t k) {
-  if (k == kBoth) {
-    const float mid = (hi + lo) * 0.5f;
-    const float s = (hi - lo) / kPi;
-    return mid + s * atanf(u / s);
-  }
-  if (k == kLow) return 0.5f * (2.0f * lo + u + sqrtf(u * u + 4.0f));
-  if (k == kHigh) return 0.5f * (2.0f * hi + u - sqrtf(u * u + 4.0f));
-  return u;
-}
-
-template <bool BOUNDED, bool LEGACY>
-__device__ __forceinline__ void adam_elem(const AdamArgs& a, float bc1, float bc2, float g,
-                                          float& u, float& m, float& v, float pold, float lo,
-                                          float hi, int8_t k, float& pnew) {
-  if (BOUNDED) g *= dpdu(LEGACY ? pold : u, lo, hi, k);
-  m = (1.0f - a.b1) * g + a.b1 * m;
-  v = (1.0f - a.b2) * (g * g) + a.b2 * v;
-  const float mhat = m / bc1;
-  const float vhat = v / bc2;
-  u = u - a.lr * mhat / (sqrtf(vhat) + a.eps);
-  pnew = BOUNDED ? inv_transform(u, lo, hi, k) : u;
-}
 
 // Small updates (all workgroups finish together) advance the step in a separate
 // one-thread kernel instead: ~1000 tickets on one address at the very end serialise in L2

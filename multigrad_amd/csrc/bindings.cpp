@@ -53,11 +53,20 @@ void smf_epilogue(torch::Tensor slab, int64_t nrows, std::vector<double> edges,
                   c10::optional<torch::Tensor> seq, c10::optional<torch::Tensor> err,
                   double timeout_s, c10::optional<torch::Tensor> advance);
 // xgmi.hip
-int64_t xgmi_alloc();
+int64_t xgmi_alloc(int64_t bytes);
+torch::Tensor xgmi_tensor(int64_t ptr, int64_t numel);
+void xgmi_twoshot(std::vector<int64_t> gbufs, std::vector<int64_t> tbufs, std::vector<int64_t> flags,
+                  int64_t rank, int64_t lo, int64_t n, int64_t total, int64_t mode,
+                  c10::optional<torch::Tensor> u, c10::optional<torch::Tensor> m,
+                  c10::optional<torch::Tensor> v, c10::optional<torch::Tensor> blo,
+                  c10::optional<torch::Tensor> bhi, c10::optional<torch::Tensor> kind,
+                  c10::optional<torch::Tensor> traj, torch::Tensor step, torch::Tensor seq,
+                  torch::Tensor err, std::vector<double> scalars);
+int64_t xgmi_twoshot_flag_bytes();
 pybind11::bytes xgmi_handle(int64_t base);
 int64_t xgmi_open(pybind11::bytes handle);
 void xgmi_close(int64_t ptr);
-void xgmi_zero(int64_t base);
+void xgmi_zero(int64_t base, int64_t bytes);
 void xgmi_free(int64_t ptr);
 void xgmi_allreduce(torch::Tensor x, std::vector<int64_t> peers, int64_t rank, torch::Tensor seq,
                     torch::Tensor err, double timeout_s);
@@ -113,11 +122,14 @@ PYBIND11_MODULE(_C, m) {
         pybind11::arg("S"), pybind11::arg("loss"), pybind11::arg("h"), pybind11::arg("peers"),
         pybind11::arg("rank"), pybind11::arg("seq"), pybind11::arg("err"), pybind11::arg("timeout_s"),
         pybind11::arg("advance") = pybind11::none());
-  m.def("xgmi_alloc", &mg::xgmi_alloc);
+  m.def("xgmi_alloc", &mg::xgmi_alloc, pybind11::arg("bytes") = 0);
+  m.def("xgmi_tensor", &mg::xgmi_tensor);
+  m.def("xgmi_twoshot", &mg::xgmi_twoshot);
+  m.def("xgmi_twoshot_flag_bytes", &mg::xgmi_twoshot_flag_bytes);
   m.def("xgmi_handle", &mg::xgmi_handle);
   m.def("xgmi_open", &mg::xgmi_open);
   m.def("xgmi_close", &mg::xgmi_close);
-  m.def("xgmi_zero", &mg::xgmi_zero);
+  m.def("xgmi_zero", &mg::xgmi_zero, pybind11::arg("base"), pybind11::arg("bytes") = 0);
   m.def("xgmi_free", &mg::xgmi_free);
   m.def("xgmi_allreduce", &mg::xgmi_allreduce);
   m.def("fused_adam", &mg::fused_adam, pybind11::arg("u"), pybind11::arg("m"), pybind11::arg("v"),

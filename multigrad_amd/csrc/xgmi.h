@@ -75,3 +75,52 @@ __device__ __forceinline__ void xgmi_block_allreduce(const XgmiPeers& peers, int
 }
 
 }  // namespace mg
+
+namespace mg {
+
+// ---------------------------------------------------------------------------- two-shot
+// Flag region of the two-shot reduce-scatter / all-gather (one per rank, uncached, IPC
+// mapped by every peer): gflag[q] = last step whose gradient rank q has published,
+// tflag[q] = last step whose parameter slice rank q has pushed, ticket = grid completion
+// counter of the local kernel.
+constexpr int kTsGflagOff = 0;
+constexpr int kTsTflagOff = 64;
+constexpr int kTsTicketOff = 128;
+constexpr int64_t kTsFlagBytes = 256;
+
+__device__ __forceinline__ unsigned* ts_gflag(char* b) {
+  return reinterpret_cast<unsigned*>(b + kTsGflagOff);
+}
+__device__ __forceinline__ unsigned* ts_tflag(char* b) {
+  return reinterpret_cast<unsigned*>(b + kTsTflagOff);
+}
+__device__ __forceinline__ unsigned* ts_ticket(char* b) {
+  return reinterpret_cast<unsigned*>(b + kTsTicketOff);
+}
+
+// Threads t < size of the calling block wait until flag[t] >= seq (monotonic sequence
+// numbers, wrap-safe difference); returns 1 (and raises *err) on a timeout.  Every thread
+// of the block must call it.
+__device__ __forceinline__ int ts_wait_all(unsigned* flags, int size, unsigned seq, int* err,
+                                           long long timeout_ticks) {
+  __shared__ int to;
+  if (threadIdx.x == 0) to = 0;
+  __syncthreads();
+  if ((int)threadIdx.x < size) {
+    const long long t0 = wall_clock64();
+    while ((int)(__hip_atomic_load(flags + threadIdx.x, __ATOMIC_ACQUIRE,
+                                   __HIP_MEMORY_SCOPE_SYSTEM) - seq) < 0) {
+      if (wall_clock64() - t0 > timeout_ticks) {
+        atomicExch(err, 1);
+        to = 1;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+  }
+  __threadfence_system();
+  __syncthreads();
+  return to;
+}
+
+}  // namespace mg

@@ -22,6 +22,7 @@
 // Used for tiny device all-reduces after a start-up self-test passes on every rank
 // (multigrad_amd/parallel/xgmi.py; MULTIGRAD_ALLREDUCE=rccl disables it); verified with two
 // processes sharing one GPU (tests/test_xgmi_gpu.py).
+#include "adam.h"
 #include "common.h"
 #include "xgmi.h"
 
@@ -49,13 +50,25 @@ static void xcheck(hipError_t e, const char* what) {
   TORCH_CHECK(e == hipSuccess, what, ": ", hipGetErrorString(e));
 }
 
-// Allocate and zero this rank's region; returns its device address.
-int64_t xgmi_alloc() {
+// Allocate and zero an uncached region of `bytes` (default: the one-shot region); returns
+// its device address.  Uncached (MTYPE UC): remote stores/loads over xGMI and local
+// accesses see each other without any cache maintenance.
+int64_t xgmi_alloc(int64_t bytes) {
+  if (bytes <= 0) bytes = kXRegionBytes;
   void* p = nullptr;
-  xcheck(hipExtMallocWithFlags(&p, kXRegionBytes, hipDeviceMallocUncached), "hipExtMallocWithFlags");
-  xcheck(hipMemset(p, 0, kXRegionBytes), "hipMemset");
+  xcheck(hipExtMallocWithFlags(&p, (size_t)bytes, hipDeviceMallocUncached), "hipExtMallocWithFlags");
+  xcheck(hipMemset(p, 0, (size_t)bytes), "hipMemset");
   xcheck(hipDeviceSynchronize(), "hipDeviceSynchronize");
   return reinterpret_cast<int64_t>(p);
+}
+
+// A float32 tensor aliasing `numel` floats at `ptr` on the current device (the caller
+// keeps the region alive for the tensor's lifetime).
+torch::Tensor xgmi_tensor(int64_t ptr, int64_t numel) {
+  int dev = 0;
+  xcheck(hipGetDevice(&dev), "hipGetDevice");
+  auto opts = torch::TensorOptions().dtype(torch::kFloat32).device(torch::kCUDA, dev);
+  return torch::from_blob(reinterpret_cast<void*>(ptr), {numel}, [](void*) {}, opts);
 }
 
 pybind11::bytes xgmi_handle(int64_t base) {
@@ -76,8 +89,9 @@ int64_t xgmi_open(pybind11::bytes handle) {
 
 // Re-zero this rank's region (flags and inboxes); the caller has drained every kernel
 // and synchronised with the peers before and after (OneShotAllReduce.reset).
-void xgmi_zero(int64_t base) {
-  xcheck(hipMemset(reinterpret_cast<void*>(base), 0, kXRegionBytes), "hipMemset");
+void xgmi_zero(int64_t base, int64_t bytes) {
+  if (bytes <= 0) bytes = kXRegionBytes;
+  xcheck(hipMemset(reinterpret_cast<void*>(base), 0, (size_t)bytes), "hipMemset");
   xcheck(hipDeviceSynchronize(), "hipDeviceSynchronize");
 }
 
@@ -101,5 +115,226 @@ void xgmi_allreduce(torch::Tensor x, std::vector<int64_t> peers, int64_t rank, t
                      (int)rank, size, x.data_ptr<float>(), (int)x.numel(),
                      reinterpret_cast<unsigned*>(seq.data_ptr<int>()), err.data_ptr<int>(), ticks);
 }
+
+
+// ============================================================================ two-shot
+// Reduce-scatter -> Adam -> all-gather of the dense gradient over peer memory, ONE launch
+// per optimizer step (reference multigrad/multigrad.py:531-532, the P-float
+// gradient Allreduce, plus the Adam update of multigrad/adam.py:52-68).
+//
+// Every rank holds three uncached, IPC-exported regions: its gradient g_r (written by the
+// VJP), its parameter vector theta_r (read by the forward) and a flag region.  Rank r owns
+// the float range [lo_r, lo_r + n_r) (1/W of the vector, ZeRO-1 optimizer state).  One
+// call on rank r, step seq:
+//
+//   block 0:  gflag_q[r] = seq on every rank q          (my gradient is complete)
+//   all blocks: wait gflag_r[q] >= seq for every q
+//   for each float4 of the owned range:                  (grid-stride, 16 B per access)
+//       g = g_0 + g_1 + ... + g_{W-1}   (peer loads over xGMI, FIXED rank order)
+//       Adam on (u, m, v) of the slice  (adam.h: the same bits as csrc/adam.hip)
+//       theta_q[i] = p for every rank q (peer stores over xGMI = the all-gather)
+//       trajectory row (owned slice)
+//   last block (grid ticket): tflag_q[r] = seq on every q, wait tflag_r[q] >= seq for all q
+//
+// The pulls (peer -> me) and pushes (me -> peer) run on all W-1 links of the fully
+// connected node at once: each link carries P/W floats of gradient and P/W floats of
+// parameters in each direction, where a single ring pushes (W-1)/W * P floats per phase
+// through ONE outgoing link per GPU.
+// The kernel returns only when every rank's slice has landed everywhere, so the next
+// forward reads complete parameters with no further synchronisation, and no rank can
+// overwrite its gradient (next VJP) while a peer still reads it.  The sequence number
+// lives in device memory (graph replayable); bounded waits raise err and NaN-poison the
+// owned slice instead of hanging.
+struct TwoShotArgs {
+  XgmiPeers g;          // peers' gradient regions (as mapped in this process)
+  XgmiPeers t;          // peers' parameter regions
+  XgmiPeers f;          // peers' flag regions
+  int rank, size;
+  int64_t lo, n;        // owned float range; lo % 4 == 0, n % 4 == 0
+  float* u;             // bounded: owned u slice; unbounded: nullptr (u = own parameters)
+  float* m;
+  float* v;
+  const float* blo;     // owned bounds (bounded modes)
+  const float* bhi;
+  const int8_t* kind;
+  float* traj;          // owned trajectory base (row r at traj + r * traj_stride) or null
+  int64_t traj_stride;
+  int* step;            // device step counter [step, ticket] (read when host_step < 0)
+  int host_step;
+  unsigned* seq;
+  int* err;
+  long long ticks;
+  float lr, b1, b2, eps;
+};
+
+constexpr int kTsThreads = 256;
+
+// MODE 0: plain sum (self-test: theta = sum of the gradients); 1: Adam, unbounded;
+// 2: Adam in bounded coordinates; 3: bounded with the reference's legacy Jacobian (Q1).
+template <int MODE>
+__global__ __launch_bounds__(kTsThreads) void xgmi_twoshot_kernel(TwoShotArgs a) {
+  constexpr bool BOUNDED = MODE >= 2;
+  constexpr bool LEGACY = MODE == 3;
+  const unsigned seq = __hip_atomic_load(a.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+  const int st = a.host_step >= 0
+                     ? a.host_step
+                     : __hip_atomic_load(a.step, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  char* me = a.f.base[a.rank];
+  if (blockIdx.x == 0) {  // my gradient is complete: the VJP ran before this launch
+    __threadfence_system();
+    if ((int)threadIdx.x < a.size)
+      __hip_atomic_store(ts_gflag(a.f.base[threadIdx.x]) + a.rank, seq, __ATOMIC_RELEASE,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  const int bad = ts_wait_all(ts_gflag(me), a.size, seq, a.err, a.ticks);
+  const float bc1 = 1.0f - powf(a.b1, (float)(st + 1));
+  const float bc2 = 1.0f - powf(a.b2, (float)(st + 1));
+  float* trow = a.traj ? a.traj + (int64_t)(st + 1) * a.traj_stride : nullptr;
+  const float* own = reinterpret_cast<const float*>(a.t.base[a.rank]) + a.lo;
+  const int64_t n4 = a.n >> 2;
+  const int64_t stride = (int64_t)gridDim.x * kTsThreads;
+  for (int64_t i = (int64_t)blockIdx.x * kTsThreads + threadIdx.x; i < n4; i += stride) {
+    const int64_t off = a.lo + 4 * i;
+    float4 g = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(a.g.base[0]) + off);
+    for (int q = 1; q < a.size; ++q) {
+      const float4 h = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(a.g.base[q]) + off);
+      g.x += h.x; g.y += h.y; g.z += h.z; g.w += h.w;
+    }
+    float4 p = g;
+    if constexpr (MODE >= 1) {
+      float4 u = BOUNDED ? reinterpret_cast<const float4*>(a.u)[i]
+                         : reinterpret_cast<const float4*>(own)[i];
+      float4 m = reinterpret_cast<const float4*>(a.m)[i];
+      float4 v = reinterpret_cast<const float4*>(a.v)[i];
+      float4 po = make_float4(0.f, 0.f, 0.f, 0.f), lo = po, hi = po;
+      char4 k = make_char4(0, 0, 0, 0);
+      if constexpr (BOUNDED) {
+        lo = reinterpret_cast<const float4*>(a.blo)[i];
+        hi = reinterpret_cast<const float4*>(a.bhi)[i];
+        k = reinterpret_cast<const char4*>(a.kind)[i];
+        if (LEGACY) po = reinterpret_cast<const float4*>(own)[i];
+      }
+      adam_elem<BOUNDED, LEGACY>(a, bc1, bc2, g.x, u.x, m.x, v.x, po.x, lo.x, hi.x, k.x, p.x);
+      adam_elem<BOUNDED, LEGACY>(a, bc1, bc2, g.y, u.y, m.y, v.y, po.y, lo.y, hi.y, k.y, p.y);
+      adam_elem<BOUNDED, LEGACY>(a, bc1, bc2, g.z, u.z, m.z, v.z, po.z, lo.z, hi.z, k.z, p.z);
+      adam_elem<BOUNDED, LEGACY>(a, bc1, bc2, g.w, u.w, m.w, v.w, po.w, lo.w, hi.w, k.w, p.w);
+      if (bad) {
+        const float nan = __builtin_nanf("");
+        u = make_float4(nan, nan, nan, nan);
+        p = u;
+      }
+      reinterpret_cast<float4*>(a.m)[i] = m;
+      reinterpret_cast<float4*>(a.v)[i] = v;
+      if constexpr (BOUNDED) reinterpret_cast<float4*>(a.u)[i] = u;
+      if (trow) reinterpret_cast<float4*>(trow)[i] = p;
+    } else if (bad) {
+      const float nan = __builtin_nanf("");
+      p = make_float4(nan, nan, nan, nan);
+    }
+    for (int q = 0; q < a.size; ++q)
+      *reinterpret_cast<float4*>(reinterpret_cast<float*>(a.t.base[q]) + off) = p;
+  }
+  // grid completion: the last block publishes "my slice is everywhere" and waits until
+  // every peer's slice has landed here
+  __threadfence_system();
+  __syncthreads();
+  __shared__ int last;
+  if (threadIdx.x == 0) {
+    const unsigned tk = atomicAdd(ts_ticket(me), 1u);
+    last = tk == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!last) return;
+  if (threadIdx.x == 0) __hip_atomic_store(ts_ticket(me), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if ((int)threadIdx.x < a.size)
+    __hip_atomic_store(ts_tflag(a.f.base[threadIdx.x]) + a.rank, seq, __ATOMIC_RELEASE,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+  ts_wait_all(ts_tflag(me), a.size, seq, a.err, a.ticks);
+  if (threadIdx.x == 0) {
+    __hip_atomic_store(a.seq, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (a.host_step < 0) __hip_atomic_store(a.step, st + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+static XgmiPeers peers_of(const std::vector<int64_t>& v) {
+  XgmiPeers p;
+  for (int r = 0; r < kXMaxRanks; ++r) p.base[r] = r < (int)v.size() ? reinterpret_cast<char*>(v[r]) : nullptr;
+  return p;
+}
+
+static float* opt_ptr(const c10::optional<torch::Tensor>& t, int64_t numel, const char* name) {
+  if (!t.has_value() || !t->defined() || t->numel() == 0) return nullptr;
+  TORCH_CHECK(t->is_cuda() && t->is_contiguous() && t->scalar_type() == at::kFloat, name,
+              ": contiguous fp32 device tensor");
+  TORCH_CHECK(numel < 0 || t->numel() >= numel, name, " too small");
+  TORCH_CHECK((reinterpret_cast<uintptr_t>(t->data_ptr()) & 15) == 0, name, " must be 16-byte aligned");
+  return t->data_ptr<float>();
+}
+
+// One two-shot step (see above).  mode: 0 sum, 1 Adam, 2 bounded Adam, 3 bounded legacy.
+// scalars: [host_step, lr, b1, b2, eps, timeout_s, traj_stride]
+void xgmi_twoshot(std::vector<int64_t> gbufs, std::vector<int64_t> tbufs, std::vector<int64_t> flags,
+                  int64_t rank, int64_t lo, int64_t n, int64_t total, int64_t mode,
+                  c10::optional<torch::Tensor> u, c10::optional<torch::Tensor> m,
+                  c10::optional<torch::Tensor> v, c10::optional<torch::Tensor> blo,
+                  c10::optional<torch::Tensor> bhi, c10::optional<torch::Tensor> kind,
+                  c10::optional<torch::Tensor> traj, torch::Tensor step, torch::Tensor seq,
+                  torch::Tensor err, std::vector<double> scalars) {
+  const int size = (int)gbufs.size();
+  TORCH_CHECK(size >= 1 && size <= kXMaxRanks && (int)tbufs.size() == size && (int)flags.size() == size,
+              "two-shot: 1..8 ranks, one region of each kind per rank");
+  TORCH_CHECK(rank >= 0 && rank < size, "bad rank");
+  TORCH_CHECK(lo >= 0 && n >= 0 && lo % 4 == 0 && n % 4 == 0 && lo + n <= total,
+              "owned range must be float4 aligned and inside the vector");
+  TORCH_CHECK(mode >= 0 && mode <= 3, "bad mode");
+  TORCH_CHECK(scalars.size() == 7, "scalars: host_step, lr, b1, b2, eps, timeout_s, traj_stride");
+  TORCH_CHECK(step.is_cuda() && step.scalar_type() == at::kInt && step.numel() >= 2, "step: [2] int32 device");
+  TORCH_CHECK(seq.is_cuda() && seq.scalar_type() == at::kInt && err.is_cuda() && err.scalar_type() == at::kInt,
+              "seq/err: int32 device");
+  TwoShotArgs a;
+  a.g = peers_of(gbufs);
+  a.t = peers_of(tbufs);
+  a.f = peers_of(flags);
+  a.rank = (int)rank;
+  a.size = size;
+  a.lo = lo;
+  a.n = n;
+  a.u = opt_ptr(u, n, "u");
+  a.m = opt_ptr(m, n, "m");
+  a.v = opt_ptr(v, n, "v");
+  a.blo = opt_ptr(blo, n, "lo");
+  a.bhi = opt_ptr(bhi, n, "hi");
+  a.kind = nullptr;
+  if (kind.has_value() && kind->defined() && kind->numel()) {
+    TORCH_CHECK(kind->is_cuda() && kind->scalar_type() == at::kChar && kind->numel() >= n, "kind: int8 [n]");
+    TORCH_CHECK((reinterpret_cast<uintptr_t>(kind->data_ptr()) & 3) == 0, "kind must be 4-byte aligned");
+    a.kind = kind->data_ptr<int8_t>();
+  }
+  a.traj = opt_ptr(traj, -1, "traj");
+  a.traj_stride = (int64_t)scalars[6];
+  TORCH_CHECK(a.traj_stride % 4 == 0, "trajectory stride must keep float4 alignment");
+  if (mode >= 1) TORCH_CHECK(a.m && a.v, "Adam modes need m and v");
+  if (mode >= 2) TORCH_CHECK(a.u && a.blo && a.bhi && a.kind, "bounded modes need u and the bounds");
+  a.step = step.data_ptr<int>();
+  a.host_step = (int)scalars[0];
+  a.lr = (float)scalars[1];
+  a.b1 = (float)scalars[2];
+  a.b2 = (float)scalars[3];
+  a.eps = (float)scalars[4];
+  a.ticks = (long long)(scalars[5] * 1e8);
+  a.seq = reinterpret_cast<unsigned*>(seq.data_ptr<int>());
+  a.err = err.data_ptr<int>();
+  const int64_t n4 = n / 4;
+  const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((n4 + kTsThreads - 1) / kTsThreads, 1024));
+  auto stream = at::hip::getCurrentHIPStream();
+  switch (mode) {
+    case 0: hipLaunchKernelGGL(xgmi_twoshot_kernel<0>, dim3(blocks), dim3(kTsThreads), 0, stream, a); break;
+    case 1: hipLaunchKernelGGL(xgmi_twoshot_kernel<1>, dim3(blocks), dim3(kTsThreads), 0, stream, a); break;
+    case 2: hipLaunchKernelGGL(xgmi_twoshot_kernel<2>, dim3(blocks), dim3(kTsThreads), 0, stream, a); break;
+    default: hipLaunchKernelGGL(xgmi_twoshot_kernel<3>, dim3(blocks), dim3(kTsThreads), 0, stream, a); break;
+  }
+}
+
+int64_t xgmi_twoshot_flag_bytes() { return kTsFlagBytes; }
 
 }  // namespace mg

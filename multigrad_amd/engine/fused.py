@@ -132,6 +132,9 @@ class FusedAdamEngine:
         # slab reduction (+ one-shot cross-rank sum) + loss in one launch
         self.fuse_epilogue = bool(_env_flag("MULTIGRAD_FUSED_EPILOGUE", True))
         self.oneshot = None
+        # two-shot xGMI reduce-scatter -> Adam -> all-gather of the dense gradient (ZeRO
+        # mode on GPUs; parallel/xgmi.py): None = RCCL collectives
+        self.twoshot = None
         nc = chunks if chunks is not None else int(os.environ.get("MULTIGRAD_CHUNKS", "0")) or None
         self.nchunks_req = nc if nc is not None else (1 if self.size == 1 else 4)
         self.comm_ag = None  # second communicator (own RCCL stream) for parameter all-gathers
@@ -168,7 +171,14 @@ class FusedAdamEngine:
             lengths = [pb[i + 1] - pb[i] for i in range(len(pb) - 1)]
         else:
             W = self.size if self.zero else 1
-            ub, pb, P_pad, lengths = plan_chunks(J, upp, W, self.nchunks_req)
+            ts = None
+            if self.zero and dev.type == "cuda":
+                # one chunk: the two-shot launch is the whole gradient exchange + update
+                ub, pb, P_pad, lengths = plan_chunks(J, upp, W, 1)
+                ts = self._connect_twoshot(P_pad)  # collective
+            if ts is None:
+                ub, pb, P_pad, lengths = plan_chunks(J, upp, W, self.nchunks_req)
+            self.twoshot = ts
         md.engine_set_chunks(ub)
         if self.size > 1 and dev.type == "cuda" and self.fuse_epilogue:
             from ..parallel.xgmi import get_oneshot
@@ -206,12 +216,20 @@ class FusedAdamEngine:
                             torch.cat([bounds.kind, torch.full((pad,), KIND_NONE, dtype=torch.int8,
                                                                device=dev)]))
         self.bounds = bounds
-        theta = torch.zeros(P_pad, **f32)
+        if self.twoshot is not None:
+            # parameters and gradient live in the exported peer-memory regions
+            theta = self.twoshot.theta
+            theta.zero_()
+            self.grad = self.twoshot.grad
+            self.grad.zero_()
+        else:
+            theta = torch.zeros(P_pad, **f32)
         theta[:P] = p0
         if bounds is not None:  # the recorded start is T^-1(T(guess)), as the reference
             theta.copy_(bounds.inverse(bounds.forward(theta)))
         self.theta = theta
-        self.grad = torch.zeros(P_pad, **f32)
+        if self.twoshot is None:
+            self.grad = torch.zeros(P_pad, **f32)
         nS = md.engine_nS()
         self.nS = nS
         self.rows = [md.engine_fwd_rows(c) for c in range(self.C)]
@@ -273,7 +291,8 @@ class FusedAdamEngine:
                     a, b = self.own[c]
                     o, n = self.loc_off[c], self.loc_len[c]
                     self.traj_loc[0, o:o + n] = theta[a:b]
-            if self.comm_ag is None and self.size > 1 and _env_flag("MULTIGRAD_AG_COMM", True):
+            if self.comm_ag is None and self.size > 1 and self.twoshot is None and \
+                    _env_flag("MULTIGRAD_AG_COMM", True):
                 self.comm_ag = self.comm.split(0)
         self._ag: List = [None] * self.C
         self.pending = False
@@ -292,6 +311,30 @@ class FusedAdamEngine:
         return self
 
     # ------------------------------------------------------------------ helpers
+    def _connect_twoshot(self, numel: int):
+        """The two-shot context for ``numel`` floats (kept across setups of the same
+        size), connecting it now if needed -- collective; None: use RCCL."""
+        from ..parallel.xgmi import connect_twoshot, twoshot_enabled
+        if not twoshot_enabled() or self.size > 8:
+            return None
+        ts = self.twoshot
+        if ts is not None and ts.numel == numel:
+            return ts
+        if ts is not None:
+            ts.close()
+        return connect_twoshot(self.comm, numel)
+
+    def _twoshot_update(self):
+        """Dense-gradient reduce-scatter + Adam on the owned slice + all-gather, one launch."""
+        a, b = self.own[0]
+        bnd = self.bounds_loc
+        mode = 1 if bnd is None else (3 if self.legacy else 2)
+        traj = None if self.traj_loc is None else self.traj_loc.reshape(-1)
+        self.twoshot.step(a, b - a, mode, m=self.m, v=self.v, u=self.u_loc, bounds=bnd,
+                          traj=traj, traj_stride=0 if traj is None else self.traj_loc.shape[1],
+                          step=self.step_dev[0], host_step=self._hstep(), lr=self.lr,
+                          b1=self.b1, b2=self.b2, eps=self.eps)
+
     def _owner_units(self, md, J):
         """Owner-mode unit bounds if the model's data placement allows it on every rank."""
         if not self.allow_owner or (self.size == 1 and not self.force_owner):
@@ -440,6 +483,11 @@ class FusedAdamEngine:
                            self.b1, self.b2, self.eps, self.bounds_loc, self.legacy,
                            traj_base=tb, traj_stride=(b - a) if tb is not None else 0,
                            host_step=self._hstep())
+        elif self.zero and self.twoshot is not None:
+            with self._ph("vjp"):
+                md.engine_vjp_into(self.theta, self.h, self.grad, chunk=0)
+            with self._ph("twoshot_rs_adam_ag"):
+                self._twoshot_update()
         elif self.zero:
             rs = []
             for c in range(self.C):
@@ -606,15 +654,18 @@ class FusedAdamEngine:
 
     def check(self, where: str = "", collective: bool = False) -> None:
         """Raise :class:`~multigrad_amd.parallel.xgmi.CollectiveTimeout` if a peer-memory
-        exchange of this engine timed out (its results are NaN-poisoned); a host sync.
+        exchange of this engine (one-shot sumstats, two-shot gradient) timed out -- its
+        results are NaN-poisoned; a host sync.
 
         ``collective=True`` all-reduces the verdict so every rank raises together (used
         where the caller goes on to a collective: ``params``, ``trajectory``,
         checkpoints, the periodic check of :meth:`run_adam`); ``last_loss`` and
         ``state_dict`` check locally."""
-        if self.oneshot is not None:
-            self.oneshot.check(where or f"engine step {self.step_host}",
-                               comm=self.comm if collective else None)
+        where = where or f"engine step {self.step_host}"
+        comm = self.comm if collective else None
+        for ctx in (self.twoshot, self.oneshot):
+            if ctx is not None:
+                ctx.check(where, comm=comm)
 
     def grad_collective_name(self) -> str:
         """Human-readable name of the per-step gradient collective (bench records)."""
@@ -622,6 +673,8 @@ class FusedAdamEngine:
             return "none (1 rank)"
         if self.owner:
             return "none: owner-local gradients, sumstat all-reduce only"
+        if self.zero and self.twoshot is not None:
+            return "xGMI two-shot kernel: reduce-scatter + Adam + all-gather in one launch (self-tested)"
         if self.zero:
             return "RCCL reduce-scatter + all-gather (ZeRO-1)"
         return "RCCL all-reduce"
@@ -753,7 +806,8 @@ class FusedAdamEngine:
                 self.step()
                 if hooks.active:
                     hooks(i, self.loss, self, self.params)
-                if err_every and self.oneshot is not None and (i + 1) % err_every == 0:
+                if err_every and (self.oneshot is not None or self.twoshot is not None) and \
+                        (i + 1) % err_every == 0:
                     self.check(collective=True)
                 if checkpoint_path and checkpoint_every and (i + 1) % checkpoint_every == 0:
                     self.save_checkpoint(checkpoint_path)

@@ -88,7 +88,7 @@ def owner_bounds(num_halos: int, npop: int, seed: int, size: int, device) -> lis
 def make_population_data(num_params: int = 10_000_000, num_halos: int = 1 << 27, seed: int = 0,
                          comm=None, device=None, nbins: int = 10, chunks: int = 1,
                          truth_offset=(0.1, 0.1), tail: str = "absolute",
-                         layout: str = "lanes", placement: str = "hashed") -> dict:
+                         layout: str = "auto", placement: str = "hashed") -> dict:
     """This rank's shard of the synthetic population-SMF data set.
 
     The global catalog (halo i: population ``hash(i) mod J``, log mass from a second hash)
@@ -105,6 +105,16 @@ def make_population_data(num_params: int = 10_000_000, num_halos: int = 1 << 27,
         non-zero only on its own populations and the engine skips the gradient collective
         (``data["owner_units"]``, see :class:`~multigrad_amd.engine.fused.FusedAdamEngine`).
 
+    ``layout`` (device layout of the shard, :class:`~multigrad_amd.ops.smf.PopulationShard`):
+    ``"auto"`` picks ``"lanes"`` (one lane per population, per-population VJP residuals)
+    for a single rank and the owner placement, where a rank holds every halo of its
+    populations (~27 per population at the headline size), and ``"tiles"`` (halo-parallel
+    forward, recomputing segmented VJP) for hashed shards on several ranks: there a rank
+    holds only ~27/W halos per population, the lanes of a 64-population group would idle on
+    their unequal local counts (the group order must be the same on every rank), and the
+    residuals would cost more HBM traffic than recomputing the few halos
+    (profiles/hashed_proxy.md).
+
     Returns a dict with the sorted device shard (``shard``), bins, volume, true
     parameters ``truth`` (interleaved, device) and a starting ``guess``; the target SMF is
     filled in by :meth:`PopulationSMFModel.set_target_from_truth`.
@@ -113,6 +123,8 @@ def make_population_data(num_params: int = 10_000_000, num_halos: int = 1 << 27,
     assert num_params % 2 == 0, "parameters come in (a, log_sigma) pairs"
     if placement not in ("hashed", "owner"):
         raise ValueError("placement must be 'hashed' or 'owner'")
+    if layout == "auto":
+        layout = "tiles" if placement == "hashed" and comm.size > 1 else "lanes"
     npop = num_params // 2
     if device is None:
         device = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() \

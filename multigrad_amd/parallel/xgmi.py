@@ -34,7 +34,8 @@ from typing import Optional
 import torch
 
 __all__ = ["OneShotAllReduce", "CollectiveTimeout", "oneshot_enabled", "oneshot_mode",
-           "connect", "get_oneshot", "maybe_oneshot", "MAX_FLOATS", "MAX_RANKS"]
+           "connect", "get_oneshot", "maybe_oneshot", "MAX_FLOATS", "MAX_RANKS", "TwoShot",
+           "connect_twoshot", "twoshot_enabled"]
 
 MAX_FLOATS = 64
 MAX_RANKS = 8
@@ -60,6 +61,8 @@ def _timeout_s() -> float:
 
 class OneShotAllReduce:
     """One rank's side of the one-shot all-reduce; build it with :func:`connect`."""
+
+    kind = "one-shot"
 
     def __init__(self, rank: int, size: int, base: int, peers, timeout_s: float = 5.0):
         self.rank, self.size = int(rank), int(size)
@@ -100,7 +103,7 @@ class OneShotAllReduce:
             bad = [r for r in range(comm.size) if int(flags[r])]
         if bad:
             raise CollectiveTimeout(
-                f"rank {self.rank}/{self.size}: one-shot xGMI exchange timed out after "
+                f"rank {self.rank}/{self.size}: {self.kind} xGMI exchange timed out after "
                 f"{self.timeout_s:g} s waiting for a peer on rank(s) {bad} (sequence {s}"
                 f"{', ' + where if where else ''}); its sums are NaN-poisoned.  A rank "
                 f"skipped a collective or fell behind by more than MULTIGRAD_ONESHOT_TIMEOUT; "
@@ -217,3 +220,164 @@ def get_oneshot(comm) -> Optional[OneShotAllReduce]:
     if ar is None:
         ar = comm._oneshot = connect(comm, _timeout_s()) or False
     return ar or None
+
+
+# ============================================================================ two-shot
+def twoshot_enabled() -> bool:
+    """Whether the ZeRO engine may sum its dense gradient with the two-shot kernel
+    (``MULTIGRAD_ALLREDUCE`` auto/oneshot and ``MULTIGRAD_TWOSHOT`` not 0)."""
+    if os.environ.get("MULTIGRAD_TWOSHOT", "1").lower() in ("0", "off", "false", "no"):
+        return False
+    return oneshot_mode() in ("auto", "oneshot")
+
+
+class TwoShot:
+    """Two-shot reduce-scatter -> Adam -> all-gather over peer memory (``csrc/xgmi.hip``).
+
+    Owns three uncached, IPC-exported regions per rank: the gradient buffer ``grad`` the
+    VJP writes, the parameter buffer ``theta`` the forward reads (both ``numel`` floats,
+    exposed as tensors aliasing the regions) and a flag region.  One :meth:`step` per
+    optimizer step pulls rank r's 1/W slice of every peer's gradient, sums it in rank order,
+    applies Adam to the slice and pushes the new parameters into every peer's ``theta``;
+    the launch returns (on the device) only when every slice has landed everywhere.
+    Build it with :func:`connect_twoshot` (collective, self-tested).
+    """
+
+    kind = "two-shot"
+
+    def __init__(self, comm, numel: int, regions, peers, timeout_s: float):
+        from ..ops._ext import ext
+        E = ext()
+        self.rank, self.size = comm.rank, comm.size
+        self.numel = int(numel)
+        self.regions = regions            # (grad, theta, flags) base addresses, this rank
+        self.gpeers, self.tpeers, self.fpeers = peers
+        self.timeout_s = float(timeout_s)
+        dev = torch.device("cuda", torch.cuda.current_device())
+        self.grad = E.xgmi_tensor(regions[0], self.numel)
+        self.theta = E.xgmi_tensor(regions[1], self.numel)
+        self.seq = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.err = torch.zeros(1, dtype=torch.int32, device=dev)
+        self._step0 = torch.zeros(2, dtype=torch.int32, device=dev)
+
+    def slice(self, rank: Optional[int] = None):
+        """Owned float range ``(lo, n)`` of ``rank`` (default: this rank)."""
+        r = self.rank if rank is None else rank
+        n = self.numel // self.size
+        return r * n, n
+
+    def step(self, lo: int, n: int, mode: int, m=None, v=None, u=None, bounds=None, traj=None,
+             traj_stride: int = 0, step: Optional[torch.Tensor] = None,
+             host_step: Optional[int] = None, lr: float = 0.0, b1: float = 0.9, b2: float = 0.999,
+             eps: float = 1e-8) -> None:
+        """Enqueue one exchange on the current stream.  ``mode`` 0: theta = sum of the
+        gradients (self-test); 1: unbounded Adam; 2/3: bounded (3: legacy Jacobian)."""
+        from ..ops._ext import ext
+        lo_b = hi_b = kind = None
+        if bounds is not None:
+            lo_b, hi_b, kind = bounds.lo, bounds.hi, bounds.kind
+        ext().xgmi_twoshot(self.gpeers, self.tpeers, self.fpeers, self.rank, int(lo), int(n),
+                           self.numel, int(mode), u, m, v, lo_b, hi_b, kind, traj,
+                           self._step0 if step is None else step, self.seq, self.err,
+                           [float(-1 if host_step is None else host_step), float(lr), float(b1),
+                            float(b2), float(eps), self.timeout_s, float(traj_stride)])
+
+    def check(self, where: str = "", comm=None) -> None:
+        OneShotAllReduce.check(self, where, comm)  # same err/seq protocol words
+
+    def ok(self) -> bool:
+        return int(self.err.item()) == 0
+
+    def self_test(self) -> bool:
+        """Two exchanges (mode 0) of rank-dependent gradients whose sums are exact in fp32:
+        every rank's ``theta`` must hold the full sum afterwards."""
+        dev = self.grad.device
+        idx = torch.arange(self.numel, device=dev, dtype=torch.float32)
+        for rep in range(2):
+            self.grad.copy_(torch.remainder(idx, 97.0) + (self.rank + 1) * (rep + 1))
+            torch.cuda.synchronize()
+            lo, n = self.slice()
+            self.step(lo, n, 0)
+            torch.cuda.synchronize()
+            want = (torch.remainder(idx, 97.0) * self.size
+                    + (rep + 1) * self.size * (self.size + 1) / 2)
+            if not torch.equal(self.theta, want):
+                return False
+        self.grad.zero_()
+        self.theta.zero_()
+        torch.cuda.synchronize()
+        return self.ok()
+
+    def reset(self, comm) -> None:
+        from ..ops._ext import ext
+        torch.cuda.synchronize()
+        comm.barrier()
+        ext().xgmi_zero(self.regions[2], ext().xgmi_twoshot_flag_bytes())
+        self.seq.zero_()
+        self.err.zero_()
+        torch.cuda.synchronize()
+        comm.barrier()
+
+    def close(self) -> None:
+        from ..ops._ext import ext
+        if not self.regions:
+            return
+        torch.cuda.synchronize()
+        E = ext()
+        for peers in (self.gpeers, self.tpeers, self.fpeers):
+            for r, p in enumerate(peers):
+                if r != self.rank and p:
+                    E.xgmi_close(p)
+        for b in self.regions:
+            E.xgmi_free(b)
+        self.regions = ()
+        self.grad = self.theta = None
+
+
+def connect_twoshot(comm, numel: int, timeout_s: Optional[float] = None,
+                    test: bool = True) -> Optional[TwoShot]:
+    """Collective: allocate, export, exchange and map the three regions of every rank,
+    then self-test; None (use RCCL) if any rank failed any phase.  ``numel`` must be a
+    multiple of ``4 * comm.size`` (float4 slices)."""
+    numel = int(numel)
+    if comm is None or comm.size < 2 or comm.size > MAX_RANKS or numel % (4 * comm.size):
+        return None
+    timeout_s = _timeout_s() if timeout_s is None else float(timeout_s)
+    E, regions, handles = None, [], None
+    try:
+        from ..ops._ext import ext
+        E = ext()
+        sizes = (4 * numel, 4 * numel, E.xgmi_twoshot_flag_bytes())
+        for nb in sizes:
+            regions.append(E.xgmi_alloc(nb))
+        handles = [bytes(E.xgmi_handle(b)) for b in regions]
+    except Exception as exc:  # noqa: BLE001
+        _debug(exc)
+        handles = None
+    allh = comm.allgather(handles)
+    ok = all(h is not None for h in allh)
+    peers = ([], [], [])
+    if ok:
+        try:
+            for k in range(3):
+                peers[k].extend(regions[k] if r == comm.rank else E.xgmi_open(allh[r][k])
+                                for r in range(comm.size))
+        except Exception as exc:  # noqa: BLE001
+            ok = False
+            _debug(exc)
+    if not all(comm.allgather(ok)):
+        if E is not None:
+            for k in range(3):
+                for r, p in enumerate(peers[k]):
+                    if r != comm.rank and p:
+                        E.xgmi_close(p)
+            for b in regions:
+                E.xgmi_free(b)
+        return None
+    ts = TwoShot(comm, numel, tuple(regions), peers, timeout_s)
+    comm.barrier()
+    ok = ts.self_test() if test else True
+    if not all(comm.allgather(bool(ok))):
+        ts.close()
+        return None
+    return ts

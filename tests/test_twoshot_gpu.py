@@ -1,0 +1,196 @@
+"""Two-shot peer-memory reduce-scatter -> Adam -> all-gather (csrc/xgmi.hip) with two
+processes sharing one MI355X: the flag protocol and rank-order sum, graph replay, the Adam
+modes against a PyTorch reference, the hashed-placement engine against the RCCL/gloo
+gradient path (bitwise), and a late peer failing loudly."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from distributed import run_distributed  # noqa: E402
+
+
+def _protocol(rank, size, numel, reps):
+    import multigrad_amd as mg
+    from multigrad_amd.parallel.xgmi import connect_twoshot
+    comm = mg.get_world_comm()
+    ts = connect_twoshot(comm, numel, timeout_s=10.0)
+    assert ts is not None
+    g = torch.Generator().manual_seed(7 + rank)
+    grads, outs = [], []
+    lo, n = ts.slice()
+    for _ in range(reps):
+        x = torch.randn(numel, generator=g)
+        grads.append(x.numpy())
+        ts.grad.copy_(x.cuda())
+        ts.step(lo, n, 0)
+        outs.append(ts.theta.cpu().numpy().copy())
+    # graph replay: sequence number and flags live in device memory
+    ts.grad.fill_(rank + 1.0)
+    torch.cuda.synchronize()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(graph):
+            ts.step(lo, n, 0)
+    torch.cuda.current_stream().wait_stream(s)
+    reps_out = []
+    for _ in range(3):
+        graph.replay()
+        reps_out.append(ts.theta.cpu().numpy().copy())
+    ok = ts.ok()
+    ts.close()
+    return grads, outs, reps_out, ok
+
+
+def test_twoshot_protocol_two_procs_one_gpu():
+    numel = 8 * 1000 + 8
+    (g0, o0, r0, ok0), (g1, o1, r1, ok1) = run_distributed(_protocol, 2, numel, 6, timeout=300)
+    assert ok0 and ok1
+    for a, b, x, y in zip(g0, g1, o0, o1):
+        np.testing.assert_array_equal(x, y)                       # same bits on every rank
+        np.testing.assert_array_equal(x, (a + b).astype(np.float32))  # rank-order fp32 sum
+    for x, y in zip(r0, r1):
+        np.testing.assert_array_equal(x, np.full(numel, 3.0, dtype=np.float32))
+        np.testing.assert_array_equal(y, x)
+
+
+def _adam_modes(rank, size):
+    import multigrad_amd as mg
+    from multigrad_amd.optim.transforms import Bounds
+    from multigrad_amd.parallel.xgmi import connect_twoshot
+    comm = mg.get_world_comm()
+    numel = 4096
+    ts = connect_twoshot(comm, numel, timeout_s=10.0)
+    lo, n = ts.slice()
+    dev = ts.grad.device
+    gen = torch.Generator().manual_seed(3)
+    theta0 = torch.randn(numel, generator=gen)
+    grads = [torch.randn(numel, generator=gen) for _ in range(2 * 3)]
+    spec = [(-3.0, 3.0) if i % 3 == 0 else (-5.0, None) if i % 3 == 1 else (None, None)
+            for i in range(numel)]
+    bnd = Bounds.from_spec(spec, numel, device=dev)
+    res = {}
+    for mode in (1, 2):
+        ts.theta.copy_(theta0.to(dev))
+        m = torch.zeros(n, device=dev)
+        v = torch.zeros(n, device=dev)
+        bl = None if mode == 1 else Bounds(bnd.lo[lo:lo + n].contiguous(), bnd.hi[lo:lo + n].contiguous(),
+                                          bnd.kind[lo:lo + n].contiguous())
+        u = None if mode == 1 else bl.forward(ts.theta[lo:lo + n]).contiguous()
+        traj = torch.zeros((4, n), device=dev)
+        step = torch.zeros(2, dtype=torch.int32, device=dev)
+        for k in range(3):
+            ts.grad.copy_(grads[2 * k + rank].to(dev))
+            ts.step(lo, n, mode, m=m, v=v, u=u, bounds=bl, traj=traj.reshape(-1), traj_stride=n,
+                    step=step, lr=0.05)
+        torch.cuda.synchronize()
+        res[mode] = (ts.theta.cpu().numpy().copy(), traj.cpu().numpy(), int(step[0]))
+    ok = ts.ok()
+    ts.close()
+    return res, ok, lo, n
+
+
+def test_twoshot_adam_modes_match_reference():
+    from multigrad_amd.ops.adam import adam_step_
+    from multigrad_amd.optim.transforms import Bounds
+    out = run_distributed(_adam_modes, 2, timeout=300)
+    numel = 4096
+    gen = torch.Generator().manual_seed(3)
+    theta0 = torch.randn(numel, generator=gen)
+    grads = [torch.randn(numel, generator=gen) for _ in range(6)]
+    spec = [(-3.0, 3.0) if i % 3 == 0 else (-5.0, None) if i % 3 == 1 else (None, None)
+            for i in range(numel)]
+    bnd = Bounds.from_spec(spec, numel)
+    for mode in (1, 2):
+        p = theta0.clone()
+        u = bnd.forward(p) if mode == 2 else p
+        m = torch.zeros(numel)
+        v = torch.zeros(numel)
+        step = torch.zeros(2, dtype=torch.int32)
+        for k in range(3):
+            g = grads[2 * k] + grads[2 * k + 1]
+            adam_step_(u, m, v, g, p if mode == 2 else None, step, 0.05, 0.9, 0.999, 1e-8,
+                       bnd if mode == 2 else None)
+        want = bnd.inverse(u) if mode == 2 else u
+        for res, ok, lo, n in out:
+            assert ok
+            theta, traj, st = res[mode]
+            assert st == 3
+            np.testing.assert_allclose(theta, want.numpy(), rtol=1e-5, atol=2e-6)  # fp32 CPU vs GPU (fma)
+            np.testing.assert_allclose(traj[3], want.numpy()[lo:lo + n], rtol=1e-5, atol=2e-6)
+        np.testing.assert_array_equal(out[0][0][mode][0], out[1][0][mode][0])
+
+
+def _engine_hashed(rank, size, twoshot, bounded):
+    os.environ["MULTIGRAD_TWOSHOT"] = "1" if twoshot else "0"
+    os.environ["MULTIGRAD_CHUNKS"] = "1"
+    import multigrad_amd as mg
+    from multigrad_amd.engine.fused import FusedAdamEngine
+    from multigrad_amd.models.population import PopulationSMFModel, make_population_data
+    comm = mg.get_world_comm()
+    dev = torch.device("cuda", 0)
+    data = make_population_data(6000, 300_000, seed=31, comm=comm, device=dev, placement="hashed")
+    model = PopulationSMFModel(aux_data=data, comm=comm)
+    model.set_target_from_truth()
+    eng = FusedAdamEngine(model)
+    bounds = None
+    if bounded:
+        g = data["guess"].cpu()
+        bounds = np.stack([g.numpy() - 0.5, g.numpy() + 0.7], 1)
+        bounds[1::4, 1] = np.inf
+    traj = eng.run_adam(data["guess"], nsteps=5, learning_rate=1e-3, param_bounds=bounds)
+    return (traj.cpu().numpy(), eng.twoshot is not None, eng.zero, data["shard"].layout,
+            eng.grad_collective_name())
+
+
+@pytest.mark.parametrize("bounded", [False, True])
+def test_engine_hashed_twoshot_matches_rccl_path(bounded):
+    ref = run_distributed(_engine_hashed, 2, False, bounded, timeout=600)
+    res = run_distributed(_engine_hashed, 2, True, bounded, timeout=600)
+    assert all(r[2] and r[3] == "tiles" for r in ref + res)
+    assert not ref[0][1] and res[0][1] and res[1][1], (ref[0][4], res[0][4])
+    np.testing.assert_array_equal(res[0][0], res[1][0])
+    np.testing.assert_array_equal(ref[0][0], ref[1][0])
+    np.testing.assert_array_equal(res[0][0], ref[0][0])  # bitwise: same sums, same Adam bits
+
+
+def _late(rank, size):
+    import time
+    import multigrad_amd as mg
+    from multigrad_amd.parallel.xgmi import CollectiveTimeout, connect_twoshot
+    comm = mg.get_world_comm()
+    ts = connect_twoshot(comm, 1024, timeout_s=0.3)
+    comm.barrier()
+    if rank == 1:
+        time.sleep(1.5)
+    ts.grad.fill_(1.0)
+    lo, n = ts.slice()
+    ts.step(lo, n, 0)
+    torch.cuda.synchronize()
+    nan_own = bool(torch.isnan(ts.theta[lo:lo + n]).all())
+    try:
+        ts.check("test")
+        raised = False
+    except CollectiveTimeout:
+        raised = True
+    ts.reset(comm)
+    ts.grad.fill_(float(rank + 1))
+    ts.step(lo, n, 0)
+    torch.cuda.synchronize()
+    after = ts.theta.cpu().numpy().copy()
+    ok = ts.ok()
+    ts.close()
+    return nan_own, raised, after, ok
+
+
+def test_twoshot_late_peer_fails_loudly():
+    (n0, e0, a0, ok0), (n1, e1, a1, ok1) = run_distributed(_late, 2, timeout=300)
+    assert n0 and e0             # rank 0 waited 0.3 s for rank 1's gradient: NaN + raise
+    np.testing.assert_array_equal(a0, np.full(1024, 3.0, dtype=np.float32))
+    np.testing.assert_array_equal(a1, a0)
+    assert ok0 and ok1
