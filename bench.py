@@ -57,6 +57,12 @@ def _args(argv=None):
                          "summed across ranks every step: the headline value), 'owner' "
                          "(catalog split by population), or 'both' (default: hashed is "
                          "'value', owner is 'owner_steps_per_s')")
+    ap.add_argument("--layout", default="auto", choices=["auto", "lanes", "tiles"],
+                    help="device layout of the halo shards (auto: lanes for one rank and the "
+                         "owner placement, tiles for hashed shards on several ranks)")
+    ap.add_argument("--lane-order", default="auto", choices=["auto", "global", "local"],
+                    help="lanes layout slot order (auto: local for hashed shards on several "
+                         "ranks, global otherwise)")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--profile-phases", action="store_true")
     return ap.parse_args(argv)
@@ -97,7 +103,9 @@ def time_placement(placement, args, comm, dev, sync):
 
     t_setup = time.perf_counter()
     data = make_population_data(args.params, args.halos, seed=1234, comm=comm, device=dev,
-                                placement=placement if comm.size > 1 else "hashed")
+                                placement=placement if comm.size > 1 else "hashed",
+                                layout=args.layout,
+                                lane_order=None if args.lane_order == "auto" else args.lane_order)
     model = PopulationSMFModel(aux_data=data, comm=comm)
     model.set_target_from_truth()
     history = args.history if args.history in ("full", "last") else int(args.history)
@@ -142,6 +150,8 @@ def time_placement(placement, args, comm, dev, sync):
         "grad_collective": engine.grad_collective_name(),
         "sumstat_allreduce": engine.sumstat_collective_name(),
         "chunks": engine.C,
+        "layout": data["shard"].layout + ("/" + data["shard"].lane_order
+                                          if data["shard"].layout == "lanes" else ""),
         "loss_first_timed": loss0,
         "loss_last": loss1,
         "setup_s": round(setup_s, 2),
@@ -221,6 +231,7 @@ def main(argv=None):
             "grad_collective": head["grad_collective"],
             "sumstat_allreduce": head["sumstat_allreduce"],
             "chunks": head["chunks"],
+            "layout": head["layout"],
         },
         "owner_steps_per_s": None if own is None else round(own["steps_per_s"], 3),
         "owner_ms_per_step": None if own is None else round(own["ms_per_step"], 4),
@@ -231,7 +242,7 @@ def main(argv=None):
     if own is not None and own is not head:
         rec["owner_config"] = {k: own[k] for k in ("parallelism", "optimizer_sharding",
                                                    "grad_collective", "sumstat_allreduce",
-                                                   "chunks", "pipelined")}
+                                                   "chunks", "pipelined", "layout")}
     if args.profile_phases:
         rec["phases_ms"] = head["phases_ms"]
         if own is not None and own is not head:

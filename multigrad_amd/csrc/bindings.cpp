@@ -47,6 +47,11 @@ void smf_vjp_adam_lanes(torch::Tensor slot_pop, torch::Tensor slot_part, torch::
                         int64_t host_step, double lr, double b1, double b2, double eps,
                         c10::optional<torch::Tensor> traj, int64_t traj_stride);
 torch::Tensor smf_fwd_trace();
+void smf_vjp_lanes_rc(torch::Tensor xi, torch::Tensor slot_idx, torch::Tensor slot_part,
+                      torch::Tensor group_base, torch::Tensor group_len, torch::Tensor theta,
+                      torch::Tensor h, std::vector<double> edges, std::vector<double> scale,
+                      bool log_sigma, int64_t g0, int64_t g1, torch::Tensor grad,
+                      torch::Tensor partials, torch::Tensor giant);
 void smf_epilogue(torch::Tensor slab, int64_t nrows, std::vector<double> edges,
                   std::vector<double> scale, torch::Tensor target, double eps, torch::Tensor S,
                   torch::Tensor loss, torch::Tensor h, std::vector<int64_t> peers, int64_t rank,
@@ -117,6 +122,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("smf_vjp_lanes", &mg::smf_vjp_lanes);
   m.def("smf_vjp_adam_lanes", &mg::smf_vjp_adam_lanes);
   m.def("smf_fwd_trace", &mg::smf_fwd_trace);
+  m.def("smf_vjp_lanes_rc", &mg::smf_vjp_lanes_rc);
   m.def("smf_epilogue", &mg::smf_epilogue, pybind11::arg("slab"), pybind11::arg("nrows"),
         pybind11::arg("edges"), pybind11::arg("scale"), pybind11::arg("target"), pybind11::arg("eps"),
         pybind11::arg("S"), pybind11::arg("loss"), pybind11::arg("h"), pybind11::arg("peers"),

@@ -1191,6 +1191,52 @@ __global__ __launch_bounds__(kThreads) void smf_vjp_lanes_kernel(
 #endif
 }
 
+// VJP by recomputation over the lanes layout (no residuals): one wavefront per 64-slot
+// group, each lane accumulates A = sum_e h_e exp2(-w^2), B = sum_e h_e exp2(-w^2) w over
+// its population's halos (halo_vjp, as the tiles VJP) and writes the population's
+// gradient -- or a partial for a split population (finalized in fixed order).  Used for
+// data-parallel "hashed" shards, where a rank holds few halos per population (~3.4 at 8
+// ranks): re-evaluating them is cheaper than writing and reading 2(NB+1) residual floats
+// per population slot (profiles/hashed_proxy.md).  Groups are visited in creation
+// (window) order, grid-strided over persistent wavefronts, so the gradient writes of one
+// window of populations stay close in time.
+template <int NB, bool LOGSIG>
+__global__ __launch_bounds__(kThreads) void smf_vjp_lanes_rc_kernel(
+    const float* __restrict__ xi, const int32_t* __restrict__ slot_idx,
+    const int32_t* __restrict__ slot_part, const int64_t* __restrict__ group_base,
+    const int32_t* __restrict__ group_len, const float2* __restrict__ theta,
+    const float* __restrict__ hvec, SmfBins bins, int64_t g0, int64_t g1,
+    float2* __restrict__ grad, float2* __restrict__ partials) {
+  float h[NB + 1];
+#pragma unroll
+  for (int e = 0; e <= NB; ++e) h[e] = hvec[e];
+  const int lane = threadIdx.x & (kWave - 1);
+  const int64_t nw = (int64_t)gridDim.x * (kThreads / kWave);
+  for (int64_t g = g0 + (int64_t)blockIdx.x * (kThreads / kWave) + (threadIdx.x >> 6); g < g1;
+       g += nw) {
+    const int64_t s = g * kWave + lane;
+    const int c = slot_idx[s];
+    const float2 th = theta[c < 0 ? 0 : c];
+    const float inv = inv_sigma<LOGSIG>(th.y) * kWScale;
+    const int len = group_len[g];
+    const float* xp = xi + group_base[g] + lane;
+    float A = 0.0f, B = 0.0f;
+    int j = 0;
+    for (; j + 2 <= len; j += 2) {
+      const float x0 = xp[(int64_t)j * kWave];
+      const float x1 = xp[(int64_t)(j + 1) * kWave];
+      halo_vjp<NB, LOGSIG>(x0, th, inv, h, bins, A, B);
+      halo_vjp<NB, LOGSIG>(x1, th, inv, h, bins, A, B);
+    }
+    if (j < len) halo_vjp<NB, LOGSIG>(xp[(int64_t)j * kWave], th, inv, h, bins, A, B);
+    if (c >= 0) {
+      const int part = slot_part[s];
+      if (part >= 0) partials[part] = make_float2(A, B);
+      else grad[c] = pop_grad<LOGSIG>(th, A, B);
+    }
+  }
+}
+
 // Interleave the population-sorted halos into the lanes layout (one wave per group).
 __global__ __launch_bounds__(kThreads) void smf_lanes_pack_kernel(
     const float* __restrict__ xs, const int64_t* __restrict__ slot_src,
@@ -1736,6 +1782,69 @@ void smf_vjp_lanes(torch::Tensor slot_pop, torch::Tensor slot_part, torch::Tenso
       hipLaunchKernelGGL((smf_vjp_finalize_kernel<true>), dim3(ng), dim3(kThreads), 0, stream, giant.data_ptr<int32_t>(), pa, tp, gp);
     else
       hipLaunchKernelGGL((smf_vjp_finalize_kernel<false>), dim3(ng), dim3(kThreads), 0, stream, giant.data_ptr<int32_t>(), pa, tp, gp);
+  }
+}
+
+
+// Recompute VJP over groups [g0, g1) of the lanes schedule (whole shard or one chunk)
+// plus the fixed-order finalize of split populations (giant [G,3]).
+void smf_vjp_lanes_rc(torch::Tensor xi, torch::Tensor slot_idx, torch::Tensor slot_part,
+                      torch::Tensor group_base, torch::Tensor group_len, torch::Tensor theta,
+                      torch::Tensor h, std::vector<double> edges, std::vector<double> scale,
+                      bool log_sigma, int64_t g0, int64_t g1, torch::Tensor grad,
+                      torch::Tensor partials, torch::Tensor giant) {
+  check_dev(xi, "xi", at::kFloat);
+  check_dev(slot_idx, "slot_idx", at::kInt);
+  check_dev(slot_part, "slot_part", at::kInt);
+  check_dev(group_base, "group_base", at::kLong);
+  check_dev(group_len, "group_len", at::kInt);
+  check_dev(theta, "theta", at::kFloat);
+  check_dev(h, "h", at::kFloat);
+  check_dev(grad, "grad", at::kFloat);
+  const int nbp = padded_bins((int)scale.size());
+  const int64_t ng = group_len.numel();
+  TORCH_CHECK(h.numel() >= nbp + 1, "h too small");
+  TORCH_CHECK(grad.numel() >= theta.numel(), "grad smaller than theta");
+  TORCH_CHECK(slot_idx.numel() == ng * kWave && slot_part.numel() == ng * kWave &&
+                  group_base.numel() == ng + 1, "inconsistent lane schedule");
+  TORCH_CHECK(g0 >= 0 && g1 <= ng && g0 <= g1, "bad group range");
+  const SmfBins b = make_bins(edges, scale, nbp);
+  auto stream = at::hip::getCurrentHIPStream();
+  const float2* tp = reinterpret_cast<const float2*>(theta.data_ptr<float>());
+  float2* gp = reinterpret_cast<float2*>(grad.data_ptr<float>());
+  float2* pa = partials.numel() ? reinterpret_cast<float2*>(partials.data_ptr<float>()) : nullptr;
+  if (g1 > g0) {
+    static int64_t caps[kMaxBins + 1] = {0};
+    int64_t& cap = caps[nbp];
+    if (cap == 0) {
+      int dev = 0, occ = 0;
+      (void)hipGetDevice(&dev);
+      hipDeviceProp_t prop;
+      (void)hipGetDeviceProperties(&prop, dev);
+      MG_DISPATCH_NB(nbp, {
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)smf_vjp_lanes_rc_kernel<NB, true>, kThreads, 0);
+      });
+      cap = (int64_t)std::max(1, occ) * prop.multiProcessorCount;
+    }
+    const int64_t want = (g1 - g0 + (kThreads / kWave) - 1) / (kThreads / kWave);
+    const int64_t nblk = std::max<int64_t>(1, std::min(cap, want));
+    MG_DISPATCH_NB(nbp, {
+      with_bool(log_sigma, [&](auto LS) {
+        hipLaunchKernelGGL((smf_vjp_lanes_rc_kernel<NB, decltype(LS)::value>), dim3(nblk), dim3(kThreads), 0,
+                           stream, xi.data_ptr<float>(), slot_idx.data_ptr<int32_t>(),
+                           slot_part.data_ptr<int32_t>(), group_base.data_ptr<int64_t>(),
+                           group_len.data_ptr<int32_t>(), tp, h.data_ptr<float>(), b, g0, g1, gp, pa);
+      });
+    });
+  }
+  const int64_t ngi = giant.numel() / 3;
+  if (ngi > 0) {
+    check_dev(giant, "giant", at::kInt);
+    TORCH_CHECK(pa != nullptr, "partials buffer required");
+    if (log_sigma)
+      hipLaunchKernelGGL((smf_vjp_finalize_kernel<true>), dim3(ngi), dim3(kThreads), 0, stream, giant.data_ptr<int32_t>(), pa, tp, gp);
+    else
+      hipLaunchKernelGGL((smf_vjp_finalize_kernel<false>), dim3(ngi), dim3(kThreads), 0, stream, giant.data_ptr<int32_t>(), pa, tp, gp);
   }
 }
 

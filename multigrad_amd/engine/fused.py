@@ -171,14 +171,10 @@ class FusedAdamEngine:
             lengths = [pb[i + 1] - pb[i] for i in range(len(pb) - 1)]
         else:
             W = self.size if self.zero else 1
-            ts = None
+            ub, pb, P_pad, lengths = plan_chunks(J, upp, W, self.nchunks_req)
+            self.twoshot = None
             if self.zero and dev.type == "cuda":
-                # one chunk: the two-shot launch is the whole gradient exchange + update
-                ub, pb, P_pad, lengths = plan_chunks(J, upp, W, 1)
-                ts = self._connect_twoshot(P_pad)  # collective
-            if ts is None:
-                ub, pb, P_pad, lengths = plan_chunks(J, upp, W, self.nchunks_req)
-            self.twoshot = ts
+                self.twoshot = self._connect_twoshot(P_pad)  # collective
         md.engine_set_chunks(ub)
         if self.size > 1 and dev.type == "cuda" and self.fuse_epilogue:
             from ..parallel.xgmi import get_oneshot
@@ -295,6 +291,14 @@ class FusedAdamEngine:
                     _env_flag("MULTIGRAD_AG_COMM", True):
                 self.comm_ag = self.comm.split(0)
         self._ag: List = [None] * self.C
+        if self.twoshot is not None:
+            # per chunk: the two-shot exchange of chunk c runs on a side stream as soon as
+            # the VJP of chunk c is done (overlapping the VJP of chunk c+1), and the next
+            # step's forward of chunk c waits only for that chunk's exchange
+            self.comm_stream = torch.cuda.Stream(device=dev)
+            self.ev_vjp = [torch.cuda.Event() for _ in range(self.C)]
+            self.ev_ts = [torch.cuda.Event() for _ in range(self.C)]
+        self._ts_pending = [False] * self.C
         self.pending = False
         ok = getattr(md, "engine_pipeline_ok", None)
         self.pipeline = bool(
@@ -318,22 +322,34 @@ class FusedAdamEngine:
         if not twoshot_enabled() or self.size > 8:
             return None
         ts = self.twoshot
+        if ts is not None:
+            torch.cuda.synchronize()  # no exchange of a previous run still in flight
         if ts is not None and ts.numel == numel:
             return ts
         if ts is not None:
             ts.close()
         return connect_twoshot(self.comm, numel)
 
-    def _twoshot_update(self):
-        """Dense-gradient reduce-scatter + Adam on the owned slice + all-gather, one launch."""
-        a, b = self.own[0]
-        bnd = self.bounds_loc
+    def _twoshot_update(self, c: int):
+        """Chunk c: dense-gradient reduce-scatter + Adam on the owned slice + all-gather,
+        one launch on the side stream after the chunk's VJP."""
+        cur = torch.cuda.current_stream()
+        self.ev_vjp[c].record(cur)
+        self.comm_stream.wait_event(self.ev_vjp[c])
+        a, b = self.own[c]
+        o, n = self.loc_off[c], self.loc_len[c]
+        bnd = self._bslice(c)
         mode = 1 if bnd is None else (3 if self.legacy else 2)
-        traj = None if self.traj_loc is None else self.traj_loc.reshape(-1)
-        self.twoshot.step(a, b - a, mode, m=self.m, v=self.v, u=self.u_loc, bounds=bnd,
-                          traj=traj, traj_stride=0 if traj is None else self.traj_loc.shape[1],
-                          step=self.step_dev[0], host_step=self._hstep(), lr=self.lr,
-                          b1=self.b1, b2=self.b2, eps=self.eps)
+        traj = None if self.traj_loc is None else self.traj_loc.reshape(-1)[o:]
+        with torch.cuda.stream(self.comm_stream):
+            self.twoshot.step(a, b - a, mode, m=self.m[o:o + n], v=self.v[o:o + n],
+                              u=None if self.u_loc is None else self.u_loc[o:o + n],
+                              bounds=bnd, traj=traj,
+                              traj_stride=0 if traj is None else self.traj_loc.shape[1],
+                              step=self.step_dev[c], host_step=self._hstep(), lr=self.lr,
+                              b1=self.b1, b2=self.b2, eps=self.eps)
+        self.ev_ts[c].record(self.comm_stream)
+        self._ts_pending[c] = True
 
     def _owner_units(self, md, J):
         """Owner-mode unit bounds if the model's data placement allows it on every rank."""
@@ -381,6 +397,9 @@ class FusedAdamEngine:
 
     def _drain(self, c):
         """Wait for chunk c's parameter all-gather (stream-ordered)."""
+        if self._ts_pending[c]:
+            torch.cuda.current_stream().wait_event(self.ev_ts[c])
+            self._ts_pending[c] = False
         w = self._ag[c]
         if w is None:
             return
@@ -484,10 +503,10 @@ class FusedAdamEngine:
                            traj_base=tb, traj_stride=(b - a) if tb is not None else 0,
                            host_step=self._hstep())
         elif self.zero and self.twoshot is not None:
-            with self._ph("vjp"):
-                md.engine_vjp_into(self.theta, self.h, self.grad, chunk=0)
-            with self._ph("twoshot_rs_adam_ag"):
-                self._twoshot_update()
+            for c in range(self.C):
+                with self._ph("vjp"):
+                    md.engine_vjp_into(self.theta, self.h, self.grad, chunk=c)
+                self._twoshot_update(c)
         elif self.zero:
             rs = []
             for c in range(self.C):

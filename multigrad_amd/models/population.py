@@ -88,7 +88,8 @@ def owner_bounds(num_halos: int, npop: int, seed: int, size: int, device) -> lis
 def make_population_data(num_params: int = 10_000_000, num_halos: int = 1 << 27, seed: int = 0,
                          comm=None, device=None, nbins: int = 10, chunks: int = 1,
                          truth_offset=(0.1, 0.1), tail: str = "absolute",
-                         layout: str = "auto", placement: str = "hashed") -> dict:
+                         layout: str = "auto", placement: str = "hashed",
+                         lane_order: Optional[str] = None) -> dict:
     """This rank's shard of the synthetic population-SMF data set.
 
     The global catalog (halo i: population ``hash(i) mod J``, log mass from a second hash)
@@ -105,15 +106,17 @@ def make_population_data(num_params: int = 10_000_000, num_halos: int = 1 << 27,
         non-zero only on its own populations and the engine skips the gradient collective
         (``data["owner_units"]``, see :class:`~multigrad_amd.engine.fused.FusedAdamEngine`).
 
-    ``layout`` (device layout of the shard, :class:`~multigrad_amd.ops.smf.PopulationShard`):
-    ``"auto"`` picks ``"lanes"`` (one lane per population, per-population VJP residuals)
-    for a single rank and the owner placement, where a rank holds every halo of its
-    populations (~27 per population at the headline size), and ``"tiles"`` (halo-parallel
-    forward, recomputing segmented VJP) for hashed shards on several ranks: there a rank
-    holds only ~27/W halos per population, the lanes of a 64-population group would idle on
-    their unequal local counts (the group order must be the same on every rank), and the
-    residuals would cost more HBM traffic than recomputing the few halos
-    (profiles/hashed_proxy.md).
+    ``layout`` (device layout of the shard, :class:`~multigrad_amd.ops.smf.PopulationShard`)
+    and ``lane_order``: ``"auto"`` picks the lanes layout (one lane per population, slots
+    in the global order, per-population VJP residuals) for a single rank and the owner
+    placement, where a rank holds every halo of its populations (~27 per population at
+    the headline size); and ``"tiles"`` (halo-parallel forward, segmented recomputing VJP)
+    for hashed shards on several ranks, where a rank holds only ~27/W halos per population:
+    there the residuals cost more HBM traffic than recomputing the few halos, and lanes
+    spend most of their time on per-group overhead.  Measured per-rank proxies at 1/8 of
+    the halos (profiles/hashed_proxy.md): tiles 94 + 63 us (forward + VJP), lanes with
+    the local slot order and the recomputing VJP (``lane_order="local"``) 120 + 136 us,
+    lanes global order with residuals 140 + 146 us.
 
     Returns a dict with the sorted device shard (``shard``), bins, volume, true
     parameters ``truth`` (interleaved, device) and a starting ``guess``; the target SMF is
@@ -125,6 +128,8 @@ def make_population_data(num_params: int = 10_000_000, num_halos: int = 1 << 27,
         raise ValueError("placement must be 'hashed' or 'owner'")
     if layout == "auto":
         layout = "tiles" if placement == "hashed" and comm.size > 1 else "lanes"
+    if lane_order is None:
+        lane_order = "global"
     npop = num_params // 2
     if device is None:
         device = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() \
@@ -150,7 +155,7 @@ def make_population_data(num_params: int = 10_000_000, num_halos: int = 1 << 27,
     logm = (10.0 - torch.log10(1.0 - q)).to(torch.float32)          # log10(1e10/(1-q))
     del idx, q
     shard = PopulationShard(logm, pop.to(torch.int32), npop, device=device, chunks=chunks,
-                            layout=layout, comm=comm)
+                            layout=layout, comm=comm, lane_order=lane_order)
     del logm, pop
     cidx = torch.arange(npop, dtype=torch.int64, device=device)
     truth = torch.empty(2 * npop, dtype=torch.float32, device=device)
@@ -235,12 +240,14 @@ class PopulationSMFModel(OnePointModel):
         return int(nz[0]), int(nz[-1]) + 1
 
     def engine_param_perm(self):
-        """Internal unit order of the engine vectors (lanes layout: populations in slot
-        order, so parameter reads and gradient writes are coalesced), or None."""
-        return self.shard.perm if self.shard.layout == "lanes" else None
+        """Internal unit order of the engine vectors (lanes layout with the global slot
+        order: populations in slot order, so parameter reads and gradient writes are
+        coalesced), or None (population order)."""
+        return self.shard.perm if self._engine_order() == "internal" else None
 
     def _engine_order(self) -> str:
-        return "internal" if self.shard.layout == "lanes" else "user"
+        sh = self.shard
+        return "internal" if sh.layout == "lanes" and sh.lane_order == "global" else "user"
 
     def engine_nS(self) -> int:
         return self.bins.nbp
@@ -254,9 +261,10 @@ class PopulationSMFModel(OnePointModel):
 
     def engine_forward_chunk(self, theta, slab, chunk=None) -> int:
         # the engine always runs the VJP of a chunk after this forward at the same theta,
-        # so the forward stores the VJP residuals (lanes layout)
-        return smf_forward_slab(theta, self.shard, self.bins, True, slab, chunk, resid=True,
-                                order=self._engine_order())
+        # so the forward stores the VJP residuals (lanes layout) -- unless the VJP
+        # recomputes (local slot order: few halos per population)
+        return smf_forward_slab(theta, self.shard, self.bins, True, slab, chunk,
+                                resid=not self.shard.vjp_recompute, order=self._engine_order())
 
     def engine_prepare(self, chunks):
         """Host-side schedule construction for the given chunks (called by the engine
@@ -268,7 +276,7 @@ class PopulationSMFModel(OnePointModel):
         """Whether :meth:`engine_forward_chunk` can also apply the previous step's VJP and
         Adam update (lanes layout on the GPU, internal order, no split populations)."""
         sh = self.shard
-        if sh.device.type != "cuda" or sh.layout != "lanes":
+        if sh.device.type != "cuda" or self._engine_order() != "internal":
             return False
         k0, k1 = (0, sh.giant.shape[0]) if chunk is None else \
             (sh.chunk_giant[chunk], sh.chunk_giant[chunk + 1])
@@ -325,7 +333,8 @@ class PopulationSMFModel(OnePointModel):
 
     def engine_vjp_into(self, theta, h, grad, chunk=None):
         return smf_vjp_into(theta, self.shard, self.bins, True, h, grad, chunk=chunk,
-                            residuals_ready=True, order=self._engine_order())
+                            residuals_ready=True, order=self._engine_order(),
+                            recompute=self.shard.vjp_recompute)
 
     def engine_vjp_adam_into(self, theta, h, m, v, unit_offset, step, host_step, lr, b1, b2,
                              eps, traj_base=None, traj_stride=0, chunk=None) -> bool:

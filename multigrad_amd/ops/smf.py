@@ -122,12 +122,19 @@ class PopulationShard:
         ``"tiles"``: halos sorted by population, segmented-scan VJP over a tile schedule
         that recomputes every halo (no residual memory).  Shared-parameter shards
         (``pop=None``) always use the plain halo array.
+    lane_order : lanes layout, how populations are grouped into 64-slot groups (sorted by
+        size within windows): ``"global"`` (default) by the cross-rank counts, so every
+        rank of a data-parallel job derives the same slot order and the engine can keep
+        its vectors in that internal order; ``"local"`` by this rank's own counts, so the
+        lanes of a group have nearly equal local lengths even when the rank holds only a
+        few halos of each population (hashed shards) -- vectors then stay in population
+        order and the VJP recomputes the halos instead of keeping residuals.
     """
 
     def __init__(self, x, pop=None, npop: int = 1, device=None, chunks: int = 1,
                  tile_halos: int = TILE_HALOS, tile_pops: int = TILE_POPS,
                  layout: str = "lanes", lane_window: int = LANE_WINDOW,
-                 lane_lmax: int = LANE_LMAX, comm=None):
+                 lane_lmax: int = LANE_LMAX, comm=None, lane_order: str = "global"):
         x = torch.as_tensor(x)
         device = torch.device(device) if device is not None else x.device
         self.device = device
@@ -138,6 +145,9 @@ class PopulationShard:
         # ordering is exercised by the multi-rank CPU tests
         self.layout = layout if pop is not None else "tiles"
         self._comm = comm
+        if lane_order not in ("global", "local"):
+            raise ValueError("lane_order must be 'global' or 'local'")
+        self.lane_order = lane_order
         self._lane_window, self._lane_lmax = int(lane_window), int(lane_lmax)
         self.resid = None          # lanes: [ngroups, 2 (nbp+1), 64] residuals of the last forward
         self.resid_epoch = 0       # bumped by every residual-writing forward
@@ -168,7 +178,7 @@ class PopulationShard:
         # the lanes population order must be identical on every rank of a data-parallel
         # job: it is decided by the cross-rank sums of the counts
         self.order_counts = None
-        if self.layout == "lanes" and comm is not None and comm.size > 1:
+        if self.layout == "lanes" and lane_order == "global" and comm is not None and comm.size > 1:
             oc = counts.clone().to(torch.int64)
             comm.all_reduce(oc)
             self.order_counts = oc
@@ -296,6 +306,12 @@ class PopulationShard:
         if self.resid is None or tuple(self.resid.shape) != shape:
             self.resid = torch.empty(shape, dtype=torch.float32, device=self.device)
         return self.resid
+
+    @property
+    def vjp_recompute(self) -> bool:
+        """Lanes layout with local slot order: the VJP re-evaluates the halos (no
+        residuals) -- the cheaper choice at few halos per population."""
+        return self.layout == "lanes" and self.lane_order == "local"
 
     def slot_index(self, order: str) -> torch.Tensor:
         """Slot -> parameter unit index for ``order`` in {"user", "internal"}."""
@@ -482,7 +498,8 @@ def smf_forward_into(theta: torch.Tensor, shard: PopulationShard, bins: SmfBins,
 
 def smf_vjp_into(theta: torch.Tensor, shard: PopulationShard, bins: SmfBins, log_sigma: bool,
                  h: torch.Tensor, grad: torch.Tensor, chunk: Optional[int] = None,
-                 residuals_ready: bool = False, order: str = "user") -> torch.Tensor:
+                 residuals_ready: bool = False, order: str = "user",
+                 recompute: bool = False) -> torch.Tensor:
     """Per-population VJP with edge weights ``h`` into ``grad`` (the chunk's parameters
     only).  CPU: autograd of the PyTorch reference restricted to the chunk's halos.
 
@@ -490,7 +507,9 @@ def smf_vjp_into(theta: torch.Tensor, shard: PopulationShard, bins: SmfBins, log
     ``residuals_ready=True`` only when the caller has just run
     ``smf_forward_*(..., resid=True)`` at this ``theta`` for this chunk (the fused engine
     does); otherwise the residual forward is recomputed here first.  ``order`` as in
-    :func:`smf_forward_slab` (``grad`` is written in the same order as ``theta``)."""
+    :func:`smf_forward_slab` (``grad`` is written in the same order as ``theta``).
+    ``recompute`` (lanes layout): re-evaluate the halos instead of reading residuals
+    (``smf_vjp_lanes_rc_kernel``)."""
     if order == "internal" and shard.layout != "lanes":
         raise ValueError("internal parameter order needs the lanes layout")
     if theta.device.type != "cuda":
@@ -517,6 +536,15 @@ def smf_vjp_into(theta: torch.Tensor, shard: PopulationShard, bins: SmfBins, log
         grad.reshape(-1)[2 * p0:2 * p1] = g[2 * p0:2 * p1].to(grad.dtype)
         return grad
     E = ext()
+    if shard.layout == "lanes" and recompute:
+        g0, g1 = shard.group_range(chunk)
+        k0, k1 = (0, shard.giant.shape[0]) if chunk is None else \
+            (shard.chunk_giant[chunk], shard.chunk_giant[chunk + 1])
+        giant = shard.giant_int if order == "internal" else shard.giant
+        E.smf_vjp_lanes_rc(shard.xi, shard.slot_index(order), shard.slot_part, shard.group_base,
+                           shard.group_len, theta, h, list(bins.edges), list(bins.scale),
+                           bool(log_sigma), g0, g1, grad, shard.partials, giant[k0:k1])
+        return grad
     if shard.layout == "lanes":
         if not residuals_ready or shard.resid is None:
             nblk = shard.fwd_blocks(1, bins.nb, log_sigma, bins.rel_tail, chunk)

@@ -126,15 +126,17 @@ def test_twoshot_adam_modes_match_reference():
         np.testing.assert_array_equal(out[0][0][mode][0], out[1][0][mode][0])
 
 
-def _engine_hashed(rank, size, twoshot, bounded):
+def _engine_hashed(rank, size, twoshot, bounded, chunks, layout="auto"):
+    lane_order = "local" if layout == "lanes" else None
     os.environ["MULTIGRAD_TWOSHOT"] = "1" if twoshot else "0"
-    os.environ["MULTIGRAD_CHUNKS"] = "1"
+    os.environ["MULTIGRAD_CHUNKS"] = str(chunks)
     import multigrad_amd as mg
     from multigrad_amd.engine.fused import FusedAdamEngine
     from multigrad_amd.models.population import PopulationSMFModel, make_population_data
     comm = mg.get_world_comm()
     dev = torch.device("cuda", 0)
-    data = make_population_data(6000, 300_000, seed=31, comm=comm, device=dev, placement="hashed")
+    data = make_population_data(6000, 300_000, seed=31, comm=comm, device=dev, placement="hashed",
+                                layout=layout, lane_order=lane_order)
     model = PopulationSMFModel(aux_data=data, comm=comm)
     model.set_target_from_truth()
     eng = FusedAdamEngine(model)
@@ -144,15 +146,24 @@ def _engine_hashed(rank, size, twoshot, bounded):
         bounds = np.stack([g.numpy() - 0.5, g.numpy() + 0.7], 1)
         bounds[1::4, 1] = np.inf
     traj = eng.run_adam(data["guess"], nsteps=5, learning_rate=1e-3, param_bounds=bounds)
-    return (traj.cpu().numpy(), eng.twoshot is not None, eng.zero, data["shard"].layout,
-            eng.grad_collective_name())
+    sh = data["shard"]
+    return (traj.cpu().numpy(), eng.twoshot is not None, eng.zero,
+            f"{sh.layout}/{sh.lane_order}" if sh.layout == "lanes" else sh.layout,
+            eng.grad_collective_name(), eng.C)
 
 
-@pytest.mark.parametrize("bounded", [False, True])
-def test_engine_hashed_twoshot_matches_rccl_path(bounded):
-    ref = run_distributed(_engine_hashed, 2, False, bounded, timeout=600)
-    res = run_distributed(_engine_hashed, 2, True, bounded, timeout=600)
-    assert all(r[2] and r[3] == "tiles" for r in ref + res)
+@pytest.mark.parametrize("bounded,chunks,layout", [(False, 1, "auto"), (True, 1, "auto"),
+                                                   (False, 3, "auto"), (True, 4, "auto"),
+                                                   (False, 2, "lanes")])
+def test_engine_hashed_twoshot_matches_rccl_path(bounded, chunks, layout):
+    """One chunk, and several chunks whose exchanges run on the side stream overlapping
+    the next chunk's VJP and the next step's forward: same bits as the RCCL/gloo path
+    (the auto layout = tiles for hashed shards, and lanes in the local slot order with the
+    recomputing VJP)."""
+    ref = run_distributed(_engine_hashed, 2, False, bounded, chunks, layout, timeout=600)
+    res = run_distributed(_engine_hashed, 2, True, bounded, chunks, layout, timeout=600)
+    want = "tiles" if layout == "auto" else "lanes/local"
+    assert all(r[2] and r[3] == want and r[5] == chunks for r in ref + res), ref[0][3]
     assert not ref[0][1] and res[0][1] and res[1][1], (ref[0][4], res[0][4])
     np.testing.assert_array_equal(res[0][0], res[1][0])
     np.testing.assert_array_equal(ref[0][0], ref[1][0])
