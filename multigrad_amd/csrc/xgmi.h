@@ -17,6 +17,27 @@ struct XgmiPeers {
   char* base[kXMaxRanks];
 };
 
+// Ordering without cache maintenance.  Every word a peer reads is in an UNCACHED region
+// (hipDeviceMallocUncached: no L2 line is ever allocated for it, on any XCD or GPU), so a
+// store is visible to every agent once memory has acknowledged it.  A release is then
+// "wait until this thread's stores are acknowledged" (s_waitcnt vmcnt(0); stores count in
+// vmcnt on gfx9) and the flag store that follows is a plain system-scope relaxed store;
+// an acquire is the polling load itself (relaxed, system scope: it bypasses the caches)
+// plus program order.  __threadfence_system() would instead write back and invalidate the
+// whole L2 of the GPU (buffer_wbl2 / buffer_inv sc0 sc1) -- on every poll iteration of the
+// acquire loads -- stalling this and every other kernel running on the chip.
+__device__ __forceinline__ void uc_release() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): all of this thread's stores acknowledged
+  asm volatile("" ::: "memory");
+}
+__device__ __forceinline__ unsigned uc_poll(const unsigned* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void uc_signal(unsigned* p, unsigned v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 __device__ __forceinline__ unsigned* xflags(char* b) {
   return reinterpret_cast<unsigned*>(b + kXFlagOff);
 }
@@ -37,11 +58,9 @@ __device__ __forceinline__ void xgmi_block_allreduce(const XgmiPeers& peers, int
       __hip_atomic_store(xdata(peers.base[p]) + (slot * kXMaxRanks + rank) * kXMaxFloats + t, mine,
                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
-  __threadfence_system();
+  uc_release();
   __syncthreads();
-  if (t < size)
-    __hip_atomic_store(xflags(peers.base[t]) + slot * kXMaxRanks + rank, seq, __ATOMIC_RELEASE,
-                       __HIP_MEMORY_SCOPE_SYSTEM);
+  if (t < size) uc_signal(xflags(peers.base[t]) + slot * kXMaxRanks + rank, seq);
   char* me = peers.base[rank];
   // a peer that never signals (a rank that skipped the call, or is late by more than the
   // timeout) must not yield a silently wrong sum: the error word is raised for the host
@@ -51,8 +70,7 @@ __device__ __forceinline__ void xgmi_block_allreduce(const XgmiPeers& peers, int
   __syncthreads();
   if (t < size) {
     const long long t0 = wall_clock64();
-    while (__hip_atomic_load(xflags(me) + slot * kXMaxRanks + t, __ATOMIC_ACQUIRE,
-                             __HIP_MEMORY_SCOPE_SYSTEM) != seq) {
+    while (uc_poll(xflags(me) + slot * kXMaxRanks + t) != seq) {
       if (wall_clock64() - t0 > timeout_ticks) {
         atomicExch(err, 1);
         timed_out = 1;
@@ -61,7 +79,7 @@ __device__ __forceinline__ void xgmi_block_allreduce(const XgmiPeers& peers, int
       __builtin_amdgcn_s_sleep(2);
     }
   }
-  __threadfence_system();
+  asm volatile("" ::: "memory");
   __syncthreads();
   if (t < n) {
     float s = 0.0f;
@@ -108,8 +126,7 @@ __device__ __forceinline__ int ts_wait_all(unsigned* flags, int size, unsigned s
   __syncthreads();
   if ((int)threadIdx.x < size) {
     const long long t0 = wall_clock64();
-    while ((int)(__hip_atomic_load(flags + threadIdx.x, __ATOMIC_ACQUIRE,
-                                   __HIP_MEMORY_SCOPE_SYSTEM) - seq) < 0) {
+    while ((int)(uc_poll(flags + threadIdx.x) - seq) < 0) {
       if (wall_clock64() - t0 > timeout_ticks) {
         atomicExch(err, 1);
         to = 1;
@@ -118,7 +135,7 @@ __device__ __forceinline__ int ts_wait_all(unsigned* flags, int size, unsigned s
       __builtin_amdgcn_s_sleep(2);
     }
   }
-  __threadfence_system();
+  asm volatile("" ::: "memory");
   __syncthreads();
   return to;
 }

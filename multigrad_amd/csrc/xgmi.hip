@@ -180,12 +180,9 @@ __global__ __launch_bounds__(kTsThreads) void xgmi_twoshot_kernel(TwoShotArgs a)
                      ? a.host_step
                      : __hip_atomic_load(a.step, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   char* me = a.f.base[a.rank];
-  if (blockIdx.x == 0) {  // my gradient is complete: the VJP ran before this launch
-    __threadfence_system();
-    if ((int)threadIdx.x < a.size)
-      __hip_atomic_store(ts_gflag(a.f.base[threadIdx.x]) + a.rank, seq, __ATOMIC_RELEASE,
-                         __HIP_MEMORY_SCOPE_SYSTEM);
-  }
+  // my gradient is complete: the VJP's stores to the uncached buffer were acknowledged
+  // before that launch ended, and this launch is ordered after it
+  if (blockIdx.x == 0 && (int)threadIdx.x < a.size) uc_signal(ts_gflag(a.f.base[threadIdx.x]) + a.rank, seq);
   const int bad = ts_wait_all(ts_gflag(me), a.size, seq, a.err, a.ticks);
   const float bc1 = 1.0f - powf(a.b1, (float)(st + 1));
   const float bc2 = 1.0f - powf(a.b2, (float)(st + 1));
@@ -234,9 +231,10 @@ __global__ __launch_bounds__(kTsThreads) void xgmi_twoshot_kernel(TwoShotArgs a)
     for (int q = 0; q < a.size; ++q)
       *reinterpret_cast<float4*>(reinterpret_cast<float*>(a.t.base[q]) + off) = p;
   }
-  // grid completion: the last block publishes "my slice is everywhere" and waits until
-  // every peer's slice has landed here
-  __threadfence_system();
+  // grid completion: every thread's pushes are acknowledged before its block takes a
+  // ticket; the last block publishes "my slice is everywhere" and waits until every
+  // peer's slice has landed here
+  uc_release();
   __syncthreads();
   __shared__ int last;
   if (threadIdx.x == 0) {
@@ -246,9 +244,7 @@ __global__ __launch_bounds__(kTsThreads) void xgmi_twoshot_kernel(TwoShotArgs a)
   __syncthreads();
   if (!last) return;
   if (threadIdx.x == 0) __hip_atomic_store(ts_ticket(me), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if ((int)threadIdx.x < a.size)
-    __hip_atomic_store(ts_tflag(a.f.base[threadIdx.x]) + a.rank, seq, __ATOMIC_RELEASE,
-                       __HIP_MEMORY_SCOPE_SYSTEM);
+  if ((int)threadIdx.x < a.size) uc_signal(ts_tflag(a.f.base[threadIdx.x]) + a.rank, seq);
   ts_wait_all(ts_tflag(me), a.size, seq, a.err, a.ticks);
   if (threadIdx.x == 0) {
     __hip_atomic_store(a.seq, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -136,6 +136,7 @@ class FusedAdamEngine:
         # mode on GPUs; parallel/xgmi.py): None = RCCL collectives
         self.twoshot = None
         nc = chunks if chunks is not None else int(os.environ.get("MULTIGRAD_CHUNKS", "0")) or None
+        self._chunks_explicit = nc is not None
         self.nchunks_req = nc if nc is not None else (1 if self.size == 1 else 4)
         self.comm_ag = None  # second communicator (own RCCL stream) for parameter all-gathers
         g = _env_flag("MULTIGRAD_GRAPH", graph)
@@ -171,10 +172,16 @@ class FusedAdamEngine:
             lengths = [pb[i + 1] - pb[i] for i in range(len(pb) - 1)]
         else:
             W = self.size if self.zero else 1
-            ub, pb, P_pad, lengths = plan_chunks(J, upp, W, self.nchunks_req)
             self.twoshot = None
             if self.zero and dev.type == "cuda":
+                # two-shot: one chunk by default -- each extra chunk is one more cross-rank
+                # rendezvous per step, and overlapping chunks needs a side stream whose
+                # event waits measured ~100 us per step (profiles/twoshot_2rank.md)
+                nch = self.nchunks_req if self._chunks_explicit else 1
+                ub, pb, P_pad, lengths = plan_chunks(J, upp, W, nch)
                 self.twoshot = self._connect_twoshot(P_pad)  # collective
+            if self.twoshot is None:
+                ub, pb, P_pad, lengths = plan_chunks(J, upp, W, self.nchunks_req)
         md.engine_set_chunks(ub)
         if self.size > 1 and dev.type == "cuda" and self.fuse_epilogue:
             from ..parallel.xgmi import get_oneshot
@@ -291,10 +298,13 @@ class FusedAdamEngine:
                     _env_flag("MULTIGRAD_AG_COMM", True):
                 self.comm_ag = self.comm.split(0)
         self._ag: List = [None] * self.C
-        if self.twoshot is not None:
-            # per chunk: the two-shot exchange of chunk c runs on a side stream as soon as
-            # the VJP of chunk c is done (overlapping the VJP of chunk c+1), and the next
-            # step's forward of chunk c waits only for that chunk's exchange
+        self.comm_stream = None
+        if self.twoshot is not None and _env_flag("MULTIGRAD_TWOSHOT_SIDE_STREAM", False):
+            # opt-in: the two-shot exchange of chunk c runs on a side stream as soon as the
+            # VJP of chunk c is done (overlapping the VJP of chunk c+1), and the next
+            # step's forward of chunk c waits only for that chunk's exchange.  Off by
+            # default: the cross-stream event waits cost more than the overlap gains on
+            # this stack (profiles/twoshot_2rank.md)
             self.comm_stream = torch.cuda.Stream(device=dev)
             self.ev_vjp = [torch.cuda.Event() for _ in range(self.C)]
             self.ev_ts = [torch.cuda.Event() for _ in range(self.C)]
@@ -306,10 +316,21 @@ class FusedAdamEngine:
             and (self.owner or (not self.zero and self.C == 1 and self.size == 1))
             and ok is not None and hasattr(md, "engine_forward_update_chunk")
             and ok(self.rank if self.owner else None))
+        # a step can be captured when every collective in it is a peer-memory kernel with
+        # its sequence number in device memory (one-shot sumstats, two-shot gradient) --
+        # RCCL/gloo calls are not captured
+        self.capturable = dev.type == "cuda" and (
+            self.size == 1 or (self.oneshot is not None and self.fuse_epilogue and
+                               (self.owner or (self.twoshot is not None and self.comm_stream is None))))
         if self._graph_auto:
             # a pipelined step is two launches (forward+update, epilogue); replaying them
-            # from a graph measured 1-5% slower than eager launches (tools/graph_ab_full.sh)
-            self.use_graph = self.size == 1 and dev.type == "cuda" and not self.pipeline
+            # from a graph measured 1-5% slower than eager launches (tools/graph_ab_full.sh).
+            # Multi-rank steps are capturable (MULTIGRAD_GRAPH=1, tested bitwise against
+            # eager) but replays measured 7x slower than the 4 eager launches of the hashed
+            # step with two ranks on one GPU (profiles/twoshot_2rank.md): eager by default.
+            self.use_graph = self.capturable and not self.pipeline and self.size == 1
+        elif self.use_graph and not self.capturable:
+            self.use_graph = False  # e.g. RCCL collectives in the step: eager launches
         self.graph = None
         self.ready = True
         return self
@@ -333,23 +354,25 @@ class FusedAdamEngine:
     def _twoshot_update(self, c: int):
         """Chunk c: dense-gradient reduce-scatter + Adam on the owned slice + all-gather,
         one launch on the side stream after the chunk's VJP."""
-        cur = torch.cuda.current_stream()
-        self.ev_vjp[c].record(cur)
-        self.comm_stream.wait_event(self.ev_vjp[c])
+        side = self.comm_stream is not None
+        if side:
+            self.ev_vjp[c].record(torch.cuda.current_stream())
+            self.comm_stream.wait_event(self.ev_vjp[c])
         a, b = self.own[c]
         o, n = self.loc_off[c], self.loc_len[c]
         bnd = self._bslice(c)
         mode = 1 if bnd is None else (3 if self.legacy else 2)
         traj = None if self.traj_loc is None else self.traj_loc.reshape(-1)[o:]
-        with torch.cuda.stream(self.comm_stream):
+        with torch.cuda.stream(self.comm_stream) if side else contextlib.nullcontext():
             self.twoshot.step(a, b - a, mode, m=self.m[o:o + n], v=self.v[o:o + n],
                               u=None if self.u_loc is None else self.u_loc[o:o + n],
                               bounds=bnd, traj=traj,
                               traj_stride=0 if traj is None else self.traj_loc.shape[1],
                               step=self.step_dev[c], host_step=self._hstep(), lr=self.lr,
                               b1=self.b1, b2=self.b2, eps=self.eps)
-        self.ev_ts[c].record(self.comm_stream)
-        self._ts_pending[c] = True
+        if side:
+            self.ev_ts[c].record(self.comm_stream)
+            self._ts_pending[c] = True
 
     def _owner_units(self, md, J):
         """Owner-mode unit bounds if the model's data placement allows it on every rank."""

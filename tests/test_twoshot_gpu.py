@@ -126,8 +126,10 @@ def test_twoshot_adam_modes_match_reference():
         np.testing.assert_array_equal(out[0][0][mode][0], out[1][0][mode][0])
 
 
-def _engine_hashed(rank, size, twoshot, bounded, chunks, layout="auto"):
+def _engine_hashed(rank, size, twoshot, bounded, chunks, layout="auto", graph=None):
     lane_order = "local" if layout == "lanes" else None
+    if graph is not None:
+        os.environ["MULTIGRAD_GRAPH"] = "1" if graph else "0"
     os.environ["MULTIGRAD_TWOSHOT"] = "1" if twoshot else "0"
     os.environ["MULTIGRAD_CHUNKS"] = str(chunks)
     import multigrad_amd as mg
@@ -149,7 +151,7 @@ def _engine_hashed(rank, size, twoshot, bounded, chunks, layout="auto"):
     sh = data["shard"]
     return (traj.cpu().numpy(), eng.twoshot is not None, eng.zero,
             f"{sh.layout}/{sh.lane_order}" if sh.layout == "lanes" else sh.layout,
-            eng.grad_collective_name(), eng.C)
+            eng.grad_collective_name(), eng.C, eng.use_graph and eng.graph is not None)
 
 
 @pytest.mark.parametrize("bounded,chunks,layout", [(False, 1, "auto"), (True, 1, "auto"),
@@ -168,6 +170,17 @@ def test_engine_hashed_twoshot_matches_rccl_path(bounded, chunks, layout):
     np.testing.assert_array_equal(res[0][0], res[1][0])
     np.testing.assert_array_equal(ref[0][0], ref[1][0])
     np.testing.assert_array_equal(res[0][0], ref[0][0])  # bitwise: same sums, same Adam bits
+
+
+@pytest.mark.parametrize("bounded", [False, True])
+def test_engine_hashed_twoshot_graph_replay_matches_eager(bounded):
+    """The whole hashed step (forward, one-shot epilogue, VJP, two-shot exchange) captured
+    into one HIP graph per rank and replayed: the same trajectory bits as eager launches."""
+    eager = run_distributed(_engine_hashed, 2, True, bounded, 1, "auto", False, timeout=600)
+    graph = run_distributed(_engine_hashed, 2, True, bounded, 1, "auto", True, timeout=600)
+    assert not eager[0][6] and graph[0][6] and graph[1][6]
+    np.testing.assert_array_equal(graph[0][0], eager[0][0])
+    np.testing.assert_array_equal(graph[1][0], eager[1][0])
 
 
 def _late(rank, size):
