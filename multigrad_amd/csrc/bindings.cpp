@@ -99,8 +99,22 @@ std::vector<torch::Tensor> lpt_waves(torch::Tensor group_len, torch::Tensor fwd_
                                      int64_t g0, int64_t g1, int64_t nwaves, double overhead);
 }  // namespace mg
 
+#ifndef MG_BUILD_HASH
+#define MG_BUILD_HASH "unknown"
+#endif
+#ifndef MG_BUILD_ARCH
+#define MG_BUILD_ARCH "unknown"
+#endif
+
 PYBIND11_MODULE(_C, m) {
   m.doc() = "multigrad_amd native extension (gfx950 HIP kernels + host runtime)";
+  m.def("build_info", []() {
+    pybind11::dict d;
+    d["source_hash"] = MG_BUILD_HASH;
+    d["offload_arch"] = MG_BUILD_ARCH;
+    d["compiled"] = __DATE__ " " __TIME__;
+    return d;
+  });
   m.def("smf_padded_bins", &mg::smf_padded_bins);
   m.def("smf_forward", &mg::smf_forward);
   m.def("smf_fwd_max_blocks", &mg::smf_fwd_max_blocks);

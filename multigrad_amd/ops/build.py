@@ -52,6 +52,23 @@ def _stale(out: str, deps: List[str]) -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
+def source_hash() -> str:
+    """SHA-1 over every native source and header (name + content), the build stamp that
+    ``_C.build_info()`` reports, so a run's records show which sources its binary came
+    from."""
+    import hashlib
+    h = hashlib.sha1()
+    for f in sorted(sources() + _headers()):
+        h.update(os.path.basename(f).encode())
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def _stamp_path() -> str:
+    return os.path.join(OBJ_DIR, "source_hash.txt")
+
+
 def _compile_cmd(src: str) -> List[str]:
     inc, _, abi = _torch_dirs()
     py_inc = sysconfig.get_paths()["include"]
@@ -59,6 +76,8 @@ def _compile_cmd(src: str) -> List[str]:
               "-DTORCH_EXTENSION_NAME=_C", "-DTORCH_API_INCLUDE_EXTENSION_H",
               "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1", "-Wno-unused-result",
               f"-I{CSRC}", f"-I{py_inc}"] + [f"-I{d}" for d in inc] + [f"-I{ROCM}/include"]
+    if os.path.basename(src) == "bindings.cpp":
+        common = common + [f'-DMG_BUILD_HASH="{source_hash()}"', f'-DMG_BUILD_ARCH="{ARCH}"']
     if src.endswith(".hip"):
         extra = os.environ.get("MULTIGRAD_HIPCC_FLAGS", "").split()
         return [os.path.join(ROCM, "bin", "hipcc"), "-c", src, "-o", _obj(src),
@@ -72,6 +91,12 @@ def build(force: bool = False, verbose: bool = False, jobs: int = 0) -> str:
     srcs = sources()
     hdrs = _headers()
     todo = [s for s in srcs if force or _stale(_obj(s), [s] + hdrs)]
+    # the stamp compiled into bindings.cpp must follow every source change
+    digest = source_hash()
+    old = open(_stamp_path()).read().strip() if os.path.exists(_stamp_path()) else ""
+    bind = [s for s in srcs if os.path.basename(s) == "bindings.cpp"]
+    if digest != old:
+        todo = sorted(set(todo) | set(bind))
     jobs = jobs or min(len(todo) or 1, int(os.environ.get("MAX_JOBS", os.cpu_count() or 4)), 8)
 
     def run(src):
@@ -101,6 +126,8 @@ def build(force: bool = False, verbose: bool = False, jobs: int = 0) -> str:
         if r.returncode != 0:
             raise RuntimeError(f"link failed\n{r.stdout}\n{r.stderr}")
         os.replace(tmp, TARGET)
+    with open(_stamp_path(), "w") as f:
+        f.write(digest)
     return TARGET
 
 

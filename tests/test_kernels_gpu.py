@@ -412,3 +412,41 @@ def test_lanes_recompute_vjp_matches_residual_vjp(giant):
     z = (torch.tensor(bins.edges, dtype=torch.float64)[None, :] - mu[:, None]) / sig[:, None]
     (g64,) = torch.autograd.grad((torch.special.ndtr(z) * hw[None, :]).sum(), th64)
     np.testing.assert_allclose(g_rc.cpu().double(), g64, rtol=2e-4, atol=2e-5 * float(g64.abs().max()))
+
+
+@pytest.mark.parametrize("mode", ["static", "dynamic"])
+def test_forward_schedules_at_eighth_shard_vs_fp64(monkeypatch, mode):
+    """The headline forward at the size of one rank of the 8-GPU owner placement (1/8 of
+    the parameters and halos): static LPT lists with the issue-priority feedback (the
+    schedule `auto` picks there) and the dynamic queues, against a float64 PyTorch oracle
+    of the same (float32-rounded) inputs; the residual VJP on a sub-sample of populations."""
+    from multigrad_amd.models.population import make_population_data
+    monkeypatch.setenv("MULTIGRAD_LPT", mode)
+    data = make_population_data(num_params=1_250_000, num_halos=1 << 24, seed=1234, device=DEV)
+    shard, bins = data["shard"], data["bins"]
+    th = data["guess"]
+    out = torch.zeros(bins.nbp, device=DEV)
+    S.smf_forward_into(th, shard, bins, True, out, resid=True)
+    # fp64 oracle on the device, in chunks of halos
+    th64 = th.double()
+    ref = torch.zeros(bins.nb, dtype=torch.float64, device=DEV)
+    for a in range(0, shard.n, 1 << 22):
+        ref += S.smf_sumstats_reference(th64, shard.x[a:a + (1 << 22)].double(),
+                                        shard.pop[a:a + (1 << 22)], bins, True)
+    np.testing.assert_allclose(out[:bins.nb].cpu().double(), ref.cpu(), rtol=2e-5)
+    # VJP through the residuals against autograd of the oracle, populations [0, 2000)
+    h = torch.linspace(0.6, -0.5, bins.nbp + 1, device=DEV)
+    grad = torch.zeros_like(th)
+    S.smf_vjp_into(th, shard, bins, True, h, grad, residuals_ready=True)
+    npop_s = 2000
+    sel = shard.pop < npop_s
+    t64 = th64[:2 * npop_s].clone().requires_grad_(True)
+    hw = h[:bins.nb + 1].double() * np.sqrt(2 * np.pi)
+    t2 = t64.reshape(-1, 2)
+    p = shard.pop[sel].long()
+    mu = shard.x[sel].double() + t2[:, 0][p]
+    sig = torch.pow(10.0, t2[:, 1][p])
+    z = (torch.tensor(bins.edges, dtype=torch.float64, device=DEV)[None, :] - mu[:, None]) / sig[:, None]
+    (g64,) = torch.autograd.grad((torch.special.ndtr(z) * hw[None, :]).sum(), t64)
+    np.testing.assert_allclose(grad[:2 * npop_s].cpu().double(), g64.cpu(), rtol=2e-4,
+                               atol=2e-5 * float(g64.abs().max()))

@@ -60,3 +60,26 @@ def test_zero_engine_schedule_over_rccl():
     traj = eng.run_adam(data["guess"], nsteps=4, learning_rate=1e-3)
     assert eng.C == 3 and eng.P_pad >= 4002
     torch.testing.assert_close(traj, ref, rtol=1e-5, atol=1e-6)
+
+
+def test_onepoint_group_on_rccl_subcommunicators(monkeypatch):
+    """OnePointGroup with each model on its own RCCL communicator and the group sum over a
+    third one (device all-reduces through RCCL, 1 rank each)."""
+    monkeypatch.setenv("MULTIGRAD_ALLREDUCE", "rccl")
+    import multigrad_amd as mg
+    from multigrad_amd.models.smf import DocsSMFModel, make_docs_data
+    dev = torch.device("cuda", 0)
+    sub_a, sub_b, main = _rccl_comm(), _rccl_comm(), _rccl_comm()
+    ma = DocsSMFModel(aux_data=make_docs_data(20_000, device=dev), comm=sub_a, device=dev)
+    mb = DocsSMFModel(aux_data=make_docs_data(30_000, true_params=(-1.9, -0.6), device=dev),
+                      comm=sub_b, device=dev)
+    grp = mg.OnePointGroup(models=(ma, mb), main_comm=main)
+    p = torch.tensor([-1.9, -0.4], device=dev)
+    loss, grad = grp.calc_loss_and_grad_from_params(p)
+    la, ga = ma.calc_loss_and_grad_from_params(p)
+    lb, gb = mb.calc_loss_and_grad_from_params(p)
+    torch.testing.assert_close(loss, la + lb)
+    torch.testing.assert_close(grad, ga + gb)
+    assert main._dev is not None and sub_a._dev is not None
+    res = grp.run_bfgs(p, maxsteps=30)
+    assert res.success or res.nit > 0
