@@ -876,6 +876,26 @@ class _EngineObjective:
         else:
             self.n_local = sum(eng.loc_len) if eng.zero else eng.P_pad
 
+    def local_box(self, param_bounds):
+        """``(lo, hi)`` of this objective's vector (user-order spec -> internal order,
+        padding unbounded, then this rank's owned slices) for the device L-BFGS-B."""
+        from ..optim.lbfgsb import bounds_arrays
+        e = self.e
+        lo_u, hi_u = bounds_arrays(param_bounds, e.P)
+        out = []
+        for arr, fill in ((lo_u, -math.inf), (hi_u, math.inf)):
+            v = torch.full((e.P_pad,), fill, dtype=torch.float32, device=self.device)
+            if arr is not None:
+                t = torch.as_tensor(arr, dtype=torch.float32, device=self.device)
+                v[:e.P] = t[e.pidx] if e.pidx is not None else t
+            if e.owner:
+                a, b = e.own_range
+                v = v[a:b]
+            elif e.zero:
+                v = torch.cat([v[a:b] for a, b in e.own])
+            out.append(v.contiguous())
+        return out[0], out[1]
+
     def x0(self) -> torch.Tensor:
         e = self.e
         if e.owner:

@@ -100,10 +100,13 @@ class _OptimizerFrontEnds:
         """L-BFGS(-B); returns a ``scipy.optimize.OptimizeResult`` on every rank.
 
         ``method="scipy"``: scipy's L-BFGS-B on the root rank, other ranks serve its
-        evaluations (the reference's protocol, exact box-constraint semantics).
-        ``method="device"``: SPMD device L-BFGS with all-reduced dot products (bounds via
-        the Adam transforms); models with the fused-engine protocol run it over the
-        ZeRO-sharded engine.  ``"auto"`` picks ``device`` above 1e5 parameters.
+        evaluations (the reference's protocol).
+        ``method="device"``: SPMD device L-BFGS with all-reduced dot products; with
+        ``param_bounds`` it is L-BFGS-B (generalized Cauchy point, subspace minimisation,
+        projected line search: :mod:`multigrad_amd.optim.lbfgsb`), so bounded fits keep
+        scipy's semantics (``bounds_mode="transform"`` uses the Adam reparameterisation
+        instead).  Models with the fused-engine protocol run it over the engine's (ZeRO-
+        or owner-) sharded vectors.  ``"auto"`` picks ``device`` above 1e5 parameters.
         """
         comm = self._opt_comm() if comm is None else comm
         x0 = as_param_tensor(guess, device=self.param_device())
@@ -114,13 +117,24 @@ class _OptimizerFrontEnds:
                                   param_bounds=param_bounds, randkey=randkey, comm=comm,
                                   device=self.param_device(), **kw)
         from ..optim import lbfgs as _lbfgs
+        from ..optim import lbfgsb as _lbfgsb
         hist = kw.pop("history", 10)
+        mode = kw.pop("bounds_mode", "project")
+        if mode not in ("project", "transform"):
+            raise ValueError("bounds_mode must be 'project' or 'transform'")
         fused = getattr(self, "fused_engine", None)
-        if fused is not None and param_bounds is None and randkey is None:
+        if fused is not None and randkey is None and (param_bounds is None or mode == "project"):
             eng = fused(comm=comm, **{k: kw.pop(k) for k in ("zero", "chunks") if k in kw})
             if eng is not None:
                 obj = eng.lbfgs_objective(x0)
-                return _lbfgs.lbfgs_minimize(obj, maxiter=maxsteps, m=hist, **kw)
+                if param_bounds is None:
+                    return _lbfgs.lbfgs_minimize(obj, maxiter=maxsteps, m=hist, **kw)
+                lo, hi = obj.local_box(param_bounds)
+                return _lbfgsb.lbfgsb_minimize(obj, lo, hi, maxiter=maxsteps, m=hist, **kw)
+        if param_bounds is not None and mode == "project":
+            return _lbfgsb.run_lbfgsb_device(self.calc_loss_and_grad_from_params, x0,
+                                             maxsteps=maxsteps, param_bounds=param_bounds,
+                                             randkey=randkey, comm=comm, history=hist, **kw)
         return _lbfgs.run_lbfgs_device(self.calc_loss_and_grad_from_params, x0, maxsteps=maxsteps,
                                        param_bounds=param_bounds, randkey=randkey, comm=comm,
                                        history=hist, **kw)

@@ -1,0 +1,452 @@
+"""Device L-BFGS-B: box-constrained L-BFGS on (optionally sharded) device vectors.
+
+The reference hands its bounds to scipy's L-BFGS-B (``multigrad/bfgs.py:83-86``).  At
+1e6-1e8 parameters that optimizer has to live on the GPUs, so this is L-BFGS-B itself
+(Byrd, Lu, Nocedal & Zhu 1995, with the projected subspace step of Morales & Nocedal
+2011, as in scipy's L-BFGS-B 3.0) in an SPMD form:
+
+* **Generalized Cauchy point.**  The first local minimiser of the quadratic model
+  ``m(x) = f + g'(x-x_k) + (x-x_k)'B(x-x_k)/2`` (compact form ``B = theta I - W M W'``,
+  ``W = [Y, theta S]``) along the projected gradient path ``P(x - t g)``.  The path
+  has one breakpoint per coordinate; each rank sends the ``K`` smallest of its own (with
+  the gradient entry and the ``2m`` row of ``W``), so every rank holds the ``K`` globally
+  smallest, sorted, and runs the same sequential segment scan on the host -- identical
+  decisions everywhere without broadcasts.  The Cauchy point is then ``P(x - t* g)``, one
+  elementwise pass on the device.  (If the minimiser lies beyond the ``K``-th breakpoint,
+  ``K`` grows and the scan repeats.)
+* **Subspace minimisation** over the free variables by the direct primal method.  The
+  ``2m x 2m`` Gram matrix of ``W`` over the free rows is the full Gram matrix (kept from
+  the history inner products) minus the rows of the active set, which are gathered; the
+  step is projected onto the box and falls back to the feasible truncation if the
+  projected step is not a descent direction.
+* **Line search** along ``d = xbar - x`` (strong Wolfe, cubic interpolation, step <= 1 so
+  the iterate stays feasible), on loss values and directional derivatives that are
+  all-reduced, i.e. bitwise identical on every rank.
+* **Host traffic.**  Two device->host copies per iteration besides the function
+  evaluations: (A) the new pair's inner products with the history together with every
+  Cauchy-point input, (B) the subspace inner products; the first evaluation of the line
+  search also carries the directional derivative at the start point.
+
+Termination as scipy: ``max|P(x-g)-x| <= pgtol`` or ``(f_k-f_{k+1})/max(|f_k|,|f_{k+1}|,1)
+<= factr * eps`` or ``maxiter``.
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional
+
+import numpy as np
+import scipy.linalg
+import scipy.optimize
+import torch
+
+from ..ops.lbfgs import MultiDot, lincomb_
+from .lbfgs import _allreduce_np, _zoom
+
+__all__ = ["lbfgsb_minimize", "run_lbfgsb_device", "BoxObjective"]
+
+_EPS = np.finfo(np.float64).eps
+
+
+class BoxObjective:
+    """Replicated objective ``loss_and_grad_fn(x) -> (loss, grad)`` in the parameters
+    themselves (no transform), for :func:`lbfgsb_minimize`."""
+
+    def __init__(self, loss_and_grad_fn, x0: torch.Tensor, comm=None, **fn_kwargs):
+        self.fn, self.kw, self.comm = loss_and_grad_fn, fn_kwargs, comm
+        self.sharded = False
+        x0 = x0.detach().reshape(-1).to(torch.float32)
+        self.device, self.shape = x0.device, x0.shape
+        self._x0 = x0.clone()
+        self.n_local = x0.numel()
+
+    def x0(self):
+        return self._x0.clone()
+
+    def full(self, x):
+        return x
+
+    def __call__(self, x):
+        loss, grad = self.fn(x, **self.kw)
+        if isinstance(loss, (tuple, list)):
+            loss = loss[0]
+        g = torch.as_tensor(grad).detach().reshape(-1).to(device=x.device, dtype=torch.float32)
+        return float(torch.as_tensor(loss).detach().double()), g.contiguous()
+
+
+def _box(lo, hi, n, device):
+    lo = torch.full((n,), -math.inf, device=device) if lo is None else \
+        torch.as_tensor(lo, dtype=torch.float32, device=device).reshape(-1).clone()
+    hi = torch.full((n,), math.inf, device=device) if hi is None else \
+        torch.as_tensor(hi, dtype=torch.float32, device=device).reshape(-1).clone()
+    return lo.contiguous(), hi.contiguous()
+
+
+class _History:
+    """m accepted (s, y) pairs in a ring of m+1 device slots (a new pair is measured in the
+    spare slot before it is accepted), with their inner products."""
+
+    def __init__(self, m: int, n: int, device):
+        self.m = int(m)
+        self.R = self.m + 1
+        self.HS = torch.zeros((2 * self.R, n), dtype=torch.float32, device=device)  # s_q, y_q
+        self.SY = np.zeros((self.R, self.R))  # s_i . y_j
+        self.SS = np.zeros((self.R, self.R))
+        self.YY = np.zeros((self.R, self.R))
+        self.order: list = []   # accepted slots, oldest first
+        self.theta = 1.0
+
+    def spare(self) -> int:
+        return min(set(range(self.R)) - set(self.order))
+
+    def s(self, q):
+        return self.HS[q]
+
+    def y(self, q):
+        return self.HS[self.R + q]
+
+    def accept(self, q: int, dots: np.ndarray) -> bool:
+        """dots[r] = (HS_r . s_q, HS_r . y_q) for every row r; decide and record."""
+        sy, yy = dots[q, 1], dots[self.R + q, 1]
+        if not (sy > _EPS * yy and yy > 0):
+            return False
+        for o in self.order + [q]:
+            self.SY[o, q] = dots[o, 1]
+            self.SY[q, o] = dots[self.R + o, 0]
+            self.SS[o, q] = self.SS[q, o] = dots[o, 0]
+            self.YY[o, q] = self.YY[q, o] = dots[self.R + o, 1]
+        self.order.append(q)
+        if len(self.order) > self.m:
+            self.order.pop(0)
+        self.theta = yy / sy
+        return True
+
+    def compact(self):
+        """``(idx, M, WWt)`` for the accepted pairs: ``M`` (2k x 2k) and the full Gram
+        matrix ``W W'`` of ``W = [Y, theta S]`` (rows in ``idx`` order)."""
+        idx = np.asarray(self.order, dtype=np.int64)
+        k = idx.size
+        if k == 0:
+            return idx, np.zeros((0, 0)), np.zeros((0, 0))
+        th = self.theta
+        sy = self.SY[np.ix_(idx, idx)]
+        D = np.diag(np.diag(sy))
+        Lm = np.tril(sy, -1)
+        ss = self.SS[np.ix_(idx, idx)]
+        K = np.block([[-D, Lm.T], [Lm, th * ss]])
+        M = np.linalg.inv(K)
+        yy = self.YY[np.ix_(idx, idx)]
+        ys = sy.T  # y_i . s_j
+        WWt = np.block([[yy, th * ys], [th * ys.T, th * th * ss]])
+        return idx, M, WWt
+
+    def rows(self, idx):
+        """Row indices of ``W = [Y_idx, S_idx]`` in HS and the theta factor per row."""
+        rows = np.concatenate([self.R + idx, idx]).astype(np.int64)
+        fac = np.concatenate([np.ones(idx.size), np.full(idx.size, self.theta)])
+        return rows, fac
+
+
+def lbfgsb_minimize(obj, lo=None, hi=None, maxiter: int = 100, m: int = 10,
+                    factr: float = 1e7, pgtol: float = 1e-5, maxls: int = 20,
+                    c1: float = 1e-4, c2: float = 0.9, K: int = 1024,
+                    callback=None, gtol: Optional[float] = None,
+                    ftol: Optional[float] = None) -> scipy.optimize.OptimizeResult:
+    """Minimise ``obj`` subject to ``lo <= x <= hi`` (local slices of the optimizer's
+    vector, +-inf allowed).  ``obj`` as for :func:`multigrad_amd.optim.lbfgs.lbfgs_minimize`
+    (``x0()``, ``__call__(x) -> (f, g)``, optional ``device_call``, ``full(x)``, ``comm``,
+    ``sharded``).  ``gtol`` / ``ftol`` are accepted as aliases of ``pgtol`` /
+    ``factr * eps`` (the unbounded driver's names)."""
+    if gtol is not None:
+        pgtol = gtol
+    if ftol is not None:
+        factr = ftol / _EPS
+    comm, sharded = obj.comm, obj.sharded
+    n = obj.n_local
+    dev = obj.device
+    lo, hi = _box(lo, hi, n, dev)
+    x = torch.minimum(torch.maximum(obj.x0().contiguous(), lo), hi)
+    f, g = obj(x)
+    g = g.clone()
+    nfev = 1
+    H = _History(m, n, dev)
+    R = H.R
+    dot = MultiDot(2 * R, n, dev)
+    dev_call = getattr(obj, "device_call", None) if dev.type == "cuda" else None
+    ftol = factr * _EPS
+    pending = None  # slot of a measured, not yet accepted pair
+    status, message, nit = 1, "STOP: TOTAL NO. of ITERATIONS REACHED LIMIT", 0
+    xt = torch.empty_like(x)
+
+    def allsum(a):
+        return _allreduce_np(comm, np.asarray(a, dtype=np.float64), sharded=sharded)
+
+    def allmax(a):
+        return _allreduce_np(comm, np.asarray(a, dtype=np.float64), op="max", sharded=sharded)
+
+    for k in range(maxiter + 1):
+        # ------------------------------------------------ copy A: pair dots + GCP inputs
+        t = torch.where(g < 0, (x - hi) / g, torch.where(g > 0, (x - lo) / g,
+                                                          torch.full_like(g, math.inf)))
+        t = torch.where(torch.isnan(t), torch.full_like(t, math.inf), t)
+        free_path = t > 0
+        d = torch.where(free_path, -g, torch.zeros_like(g))
+        pg = (torch.minimum(torch.maximum(x - g, lo), hi) - x).abs()
+        vecs = [d] if pending is None else [H.s(pending), H.y(pending), d]
+        dots_dev = dot(H.HS, 2 * R, vecs)
+        kk = min(K, n)
+        tc = torch.where(free_path & torch.isfinite(t), t, torch.full_like(t, math.inf))
+        cand_t, cand_i = torch.topk(tc, kk, largest=False, sorted=False) if kk else \
+            (tc[:0], torch.zeros(0, dtype=torch.int64, device=dev))
+        cand = torch.cat([cand_t.reshape(1, -1), g[cand_i].reshape(1, -1),
+                          H.HS[:, cand_i]], 0).double()
+        scal = torch.stack([(d.double() * d.double()).sum(),
+                            pg.max().double() if n else torch.zeros((), dtype=torch.float64,
+                                                                    device=dev),
+                            torch.isfinite(tc).sum().double()])
+        packA = torch.cat([scal, dots_dev.reshape(-1), cand.reshape(-1)]).cpu().numpy()
+        dd_l, pg_l, nfin_l = packA[:3]
+        nd = dots_dev.numel()
+        dots_l = packA[3:3 + nd].reshape(2 * R, len(vecs))
+        cand_l = packA[3 + nd:].reshape(2 + 2 * R, kk)
+        red = allsum(np.concatenate([[dd_l], dots_l.reshape(-1)]))
+        dd, dots_np = red[0], red[1:].reshape(2 * R, len(vecs))
+        pgmax = float(allmax([pg_l])[0])
+        if pending is not None:
+            H.accept(pending, dots_np[:, :2])
+            pending = None
+        Wd = dots_np[:, -1]  # HS rows . d
+        if k > 0 and callback is not None:
+            callback(obj.full(x))
+        if pgmax <= pgtol:
+            status, message = 0, "CONVERGENCE: NORM_OF_PROJECTED_GRADIENT_<=_PGTOL"
+            break
+        if k == maxiter:
+            break
+        # breakpoints: the union of every rank's kk smallest is exact up to the smallest
+        # "largest gathered" value of the ranks that had more than kk
+        blocks = comm.allgather((cand_l, int(nfin_l))) if (sharded and comm is not None and
+                                                            comm.size > 1) else [(cand_l, int(nfin_l))]
+        t_cut = math.inf
+        for cb, nf in blocks:
+            if nf > cb.shape[1]:
+                t_cut = min(t_cut, float(cb[0].max()))
+        cand_all = np.concatenate([cb for cb, _ in blocks], 1)
+        cand_all = cand_all[:, cand_all[0] <= t_cut]
+        # ------------------------------------------------ generalized Cauchy point (host)
+        idx, M, WWt = H.compact()
+        rows, fac = H.rows(idx)
+        th = H.theta
+        tstar, cvec = _cauchy_scan(dd, Wd[rows] * fac, M, th, cand_all, rows, fac,
+                                   complete=not np.isfinite(t_cut))
+        if tstar is None:  # more breakpoints before the minimiser than gathered: grow K
+            K = 8 * K      # and redo this iteration's Cauchy point (state unchanged)
+            continue
+        xcp = torch.minimum(torch.maximum(x - tstar * g, lo), hi)
+        free = (xcp > lo) & (xcp < hi)
+        # ------------------------------------------------ copy B: subspace inner products
+        kk2 = idx.size
+        if kk2:
+            Mc = M @ cvec
+            coef = np.zeros(2 * R)
+            coef[rows] = Mc * fac
+            wmc = torch.empty_like(x)
+            lincomb_(H.HS, 2 * R, torch.from_numpy(coef.astype(np.float32)).to(dev), 0.0, None, wmc)
+            r = g + th * (xcp - x) - wmc
+        else:
+            r = g + th * (xcp - x)
+        rF = torch.where(free, r, torch.zeros_like(r))
+        act = torch.nonzero(~free).reshape(-1)
+        WtZr = dot(H.HS, 2 * R, [rF])[:, 0]
+        WA = H.HS[torch.as_tensor(rows, device=dev)][:, act].double() if kk2 else \
+            torch.zeros((0, act.numel()), dtype=torch.float64, device=dev)
+        GA = WA @ WA.T
+        packB = torch.cat([WtZr.reshape(-1), GA.reshape(-1)]).cpu().numpy()
+        redB = allsum(packB)
+        WtZr_np = redB[:2 * R]
+        GA_np = redB[2 * R:].reshape(kk2 * 2, kk2 * 2) if kk2 else np.zeros((0, 0))
+        if kk2:
+            fw = fac[:, None] * fac[None, :]
+            GF = WWt - GA_np * fw               # Gram of W over the free rows
+            v = M @ (WtZr_np[rows] * fac)
+            N = np.eye(2 * kk2) - (M @ GF) / th
+            v = scipy.linalg.solve(N, v)
+            coef = np.zeros(2 * R)
+            coef[rows] = v * fac
+            zwv = torch.empty_like(x)
+            lincomb_(H.HS, 2 * R, torch.from_numpy(coef.astype(np.float32)).to(dev), 0.0, None, zwv)
+            du = -(rF / th) - (zwv / (th * th))
+        else:
+            du = -(rF / th)
+        du = torch.where(free, du, torch.zeros_like(du))
+        xbar = torch.minimum(torch.maximum(xcp + du, lo), hi)
+        dirn = xbar - x
+        # ------------------------------------------------ line search along x + a dirn
+        a1 = 1.0
+        if k == 0 or not H.order:
+            dnorm2 = float(allsum([(dirn.double() ** 2).sum().item()])[0])
+            a1 = min(1.0, 1.0 / math.sqrt(max(dnorm2, 1e-300)))
+        cache = {}
+        d0_box = [None]
+
+        def phi(alpha):
+            nonlocal nfev
+            torch.add(x, dirn, alpha=float(alpha), out=xt)
+            if dev_call is not None:
+                lt, ga = dev_call(xt)
+                ga = ga.clone()
+                parts = [lt.reshape(1).double(), (ga.double() * dirn.double()).sum().reshape(1)]
+                if d0_box[0] is None:
+                    parts.append((g.double() * dirn.double()).sum().reshape(1))
+                vals = torch.cat(parts).cpu().numpy()
+                fa = float(vals[0])
+                red2 = allsum(vals[1:])
+            else:
+                fa, ga = obj(xt)
+                ga = ga.clone()
+                parts = [(ga.double() * dirn.double()).sum().item()]
+                if d0_box[0] is None:
+                    parts.append((g.double() * dirn.double()).sum().item())
+                red2 = allsum(parts)
+            if d0_box[0] is None:
+                d0_box[0] = float(red2[1])
+            nfev += 1
+            cache[alpha] = (fa, ga, float(red2[0]))
+            return fa, float(red2[0])
+
+        best = _line_search(phi, f, d0_box, a1, c1, c2, maxls)
+        if d0_box[0] is not None and d0_box[0] >= 0:
+            # the projected subspace step is not a descent direction: truncate instead
+            ratio = torch.where(du > 0, (hi - xcp) / du, torch.where(du < 0, (lo - xcp) / du,
+                                                                    torch.full_like(du, math.inf)))
+            rmin_l = float(ratio.min().item()) if ratio.numel() else math.inf
+            rmin = -float(allmax([-rmin_l])[0])
+            dirn = xcp + min(1.0, rmin) * du - x
+            cache.clear()
+            d0_box[0] = None
+            best = _line_search(phi, f, d0_box, a1, c1, c2, maxls)
+        if best is None or best not in cache:
+            cands = [(v[0], a) for a, v in cache.items() if v[0] < f]
+            if not cands:
+                status, message = 2, "ABNORMAL_TERMINATION_IN_LNSRCH"
+                break
+            best = min(cands)[1]
+        f_new, g_new, _ = cache[best]
+        q = H.spare()
+        torch.mul(dirn, best, out=H.HS[q])
+        torch.sub(g_new, g, out=H.HS[R + q])
+        x.add_(H.HS[q])
+        x.copy_(torch.minimum(torch.maximum(x, lo), hi))
+        pending = q
+        nit = k + 1
+        f_old, f, g = f, f_new, g_new
+        if (f_old - f) <= ftol * max(abs(f_old), abs(f), 1.0):
+            status, message = 0, "CONVERGENCE: REL_REDUCTION_OF_F_<=_FACTR*EPSMCH"
+            if callback is not None:
+                callback(obj.full(x))
+            break
+    xf = obj.full(x)
+    if getattr(obj, "finalize", None) is not None:
+        xf = obj.finalize(x)
+    return scipy.optimize.OptimizeResult(
+        x=xf, fun=f, jac=g, nit=nit, nfev=nfev, njev=nfev, status=status,
+        success=status == 0, message=message)
+
+
+def _cauchy_scan(dd, p, M, theta, cand, rows, fac, complete: bool):
+    """Segment scan of the projected-gradient path (Byrd et al. 1995, algorithm CP).
+
+    ``p = W'd`` (2k), ``cand`` rows: [t, g, HS rows...] for breakpoints (any order).
+    Returns ``(t*, c)`` or ``(None, None)`` when the gathered breakpoints end before the
+    minimiser and more exist (``complete`` False)."""
+    fp = -dd
+    fpp = theta * dd - (p @ M @ p if p.size else 0.0)
+    c = np.zeros_like(p)
+    dtmin = -fp / fpp if fpp > 0 else math.inf
+    told = 0.0
+    order = np.argsort(cand[0], kind="stable")
+    Mp = M @ p if p.size else p
+    Mc = np.zeros_like(p)
+    broke = False
+    for j in order:
+        tb = cand[0, j]
+        if not np.isfinite(tb):
+            break
+        dt = tb - told
+        if dtmin < dt:
+            broke = True
+            break
+        gb = cand[1, j]
+        wb = cand[2 + rows, j] * fac if p.size else p
+        zb = -tb * gb
+        c = c + dt * p
+        Mc = Mc + dt * Mp
+        Mw = M @ wb if p.size else wb
+        fp = fp + dt * fpp + gb * gb + theta * gb * zb - (gb * (wb @ Mc) if p.size else 0.0)
+        fpp = fpp - theta * gb * gb - (2 * gb * (wb @ Mp) + gb * gb * (wb @ Mw) if p.size else 0.0)
+        p = p + gb * wb
+        Mp = Mp + gb * Mw
+        dtmin = -fp / fpp if fpp > 0 else math.inf
+        told = tb
+    if not broke and not complete:
+        return None, None
+    dtmin = max(dtmin, 0.0)
+    if not np.isfinite(dtmin):
+        dtmin = 0.0 if told > 0 else 1.0
+    c = c + dtmin * p
+    return told + dtmin, c
+
+
+def _line_search(phi, f0, d0_box, a1, c1, c2, maxls):
+    """Strong-Wolfe search on (0, 1] (bracketing + zoom); ``d0_box[0]`` is filled by the
+    first evaluation (the directional derivative at 0 travels with it)."""
+    alpha = a1
+    fa, da = phi(alpha)
+    d0 = d0_box[0]
+    if d0 >= 0:
+        return None
+    a_prev, f_prev, dphi_prev = 0.0, f0, d0
+    for i in range(maxls):
+        if i > 0:
+            fa, da = phi(alpha)
+        if not np.isfinite(fa) or fa > f0 + c1 * alpha * d0 or (i > 0 and fa >= f_prev):
+            return _zoom(phi, a_prev, alpha, f_prev, fa, dphi_prev, da, f0, d0, c1, c2, maxls)
+        if abs(da) <= -c2 * d0:
+            return alpha
+        if da >= 0 or alpha >= 1.0:
+            if da >= 0:
+                return _zoom(phi, alpha, a_prev, fa, f_prev, da, dphi_prev, f0, d0, c1, c2, maxls)
+            return alpha  # the step to the projected point: accept (sufficient decrease holds)
+        a_prev, f_prev, dphi_prev = alpha, fa, da
+        alpha = min(1.0, alpha * 2.0)
+    return None
+
+
+def run_lbfgsb_device(loss_and_grad_fn, params, maxsteps: int = 100, param_bounds=None,
+                      randkey=None, comm=None, history: int = 10, **kw):
+    """Device L-BFGS-B for a generic ``loss_and_grad_fn(params[, randkey])`` (replicated)."""
+    from ..utils.random import init_randkey
+    from ..utils.tensors import as_param_tensor
+    x0 = as_param_tensor(params)
+    lo, hi = bounds_arrays(param_bounds, x0.numel())
+    fkw = {} if randkey is None else {"randkey": init_randkey(randkey)}
+    obj = BoxObjective(loss_and_grad_fn, x0, comm=comm, **fkw)
+    return lbfgsb_minimize(obj, lo, hi, maxiter=maxsteps, m=history, **kw)
+
+
+def bounds_arrays(param_bounds, n: int):
+    """``(lo, hi)`` float arrays (+-inf for open sides) from a reference-style spec
+    ``(ndim, 2)`` with ``None`` entries, or ``(None, None)``."""
+    if param_bounds is None:
+        return None, None
+    lo = np.full(n, -np.inf)
+    hi = np.full(n, np.inf)
+    for i, b in enumerate(param_bounds):
+        if b is None:
+            continue
+        a, c = b
+        if a is not None:
+            lo[i] = float(a)
+        if c is not None:
+            hi[i] = float(c)
+    return lo.astype(np.float32), hi.astype(np.float32)

@@ -113,3 +113,113 @@ def test_sharded_lbfgs_owner_placement_matches_single_rank():
         np.testing.assert_allclose(x, x1, rtol=1e-3, atol=1e-4)
         assert f == pytest.approx(f1, rel=1e-2, abs=1e-9)
     np.testing.assert_array_equal(res[0][0], res[1][0])
+
+
+# ---------------------------------------------------------------- device L-BFGS-B
+from multigrad_amd.optim import lbfgsb as LB  # noqa: E402
+
+
+def _bounded_problem(n, seed=0):
+    rng = np.random.default_rng(seed)
+    c = rng.normal(size=n)
+    a = 0.5 + rng.random(n)
+    lo = np.where(rng.random(n) < 0.5, c - 0.3 * rng.random(n), -np.inf)
+    hi = np.where(rng.random(n) < 0.5, c + 0.3 * rng.random(n), np.inf)
+    c2 = c + np.where(rng.random(n) < 0.3, 1.0, 0.0) * np.sign(rng.normal(size=n))
+
+    def f_np(x):
+        r = x - c2
+        s = x.sum() / n
+        g = 2 * a * r + 20 * s / n + 0.25 * (np.concatenate([[0], r[:-1]]) + np.concatenate([r[1:], [0]]))
+        return float((a * r * r).sum() + 10 * s * s + 0.25 * (r[1:] * r[:-1]).sum()), g
+
+    def lg(x):
+        f, g = f_np(x.detach().double().cpu().numpy())
+        return torch.tensor(f, dtype=torch.float64), torch.from_numpy(g).float()
+
+    return lo, hi, f_np, lg
+
+
+def test_lbfgsb_matches_scipy_on_bounded_1e4_problem():
+    """1e4 coupled parameters, ~half with a bound, ~30% active at the optimum: x and f
+    of scipy's L-BFGS-B (float64) reproduced by the device L-BFGS-B (float32)."""
+    n = 10_000
+    lo, hi, f_np, lg = _bounded_problem(n)
+    x0 = np.clip(np.zeros(n), lo, hi)
+    ref = scipy.optimize.minimize(f_np, x0, jac=True, method="L-BFGS-B",
+                                  bounds=list(zip(lo, hi)), options=dict(maxiter=500))
+    res = LB.run_lbfgsb_device(lg, torch.tensor(x0, dtype=torch.float32), maxsteps=500,
+                               param_bounds=list(zip(lo, hi)))
+    assert res.success, res.message
+    assert res.fun == pytest.approx(ref.fun, rel=1e-7)
+    np.testing.assert_allclose(res.x.numpy(), ref.x, atol=1e-4)
+    x = res.x.numpy()
+    assert (x >= lo.astype(np.float32)).all() and (x <= hi.astype(np.float32)).all()
+    active = (np.abs(ref.x - lo) < 1e-9) | (np.abs(ref.x - hi) < 1e-9)
+    assert active.mean() > 0.1
+    assert abs(res.nit - ref.nit) <= 5
+
+
+def test_lbfgsb_small_breakpoint_budget_grows():
+    """A gathered-breakpoint budget far below the number of breakpoints on the path
+    (K=4) must give the same result (the scan asks for more)."""
+    n = 300
+    lo, hi, f_np, lg = _bounded_problem(n, seed=2)
+    x0 = torch.tensor(np.clip(np.zeros(n), lo, hi), dtype=torch.float32)
+    obj = LB.BoxObjective(lg, x0)
+    a = LB.lbfgsb_minimize(obj, torch.tensor(lo, dtype=torch.float32),
+                           torch.tensor(hi, dtype=torch.float32), maxiter=200, K=4)
+    b = LB.lbfgsb_minimize(obj, torch.tensor(lo, dtype=torch.float32),
+                           torch.tensor(hi, dtype=torch.float32), maxiter=200)
+    assert a.fun == pytest.approx(b.fun, rel=1e-7)
+
+
+def _docs_bounded(rank, size, method):
+    data = make_docs_data(comm=mg.get_world_comm(), device="cpu")
+    model = DocsSMFModel(aux_data=data, device="cpu", dtype=torch.float64)
+    bounds = [(-1.95, -1.0), (-1.0, 0.0)]          # the truth (-2, -0.5) is cut off in log_f
+    res = model.run_bfgs(torch.tensor([-1.2, -0.1], dtype=torch.float64), param_bounds=bounds,
+                         method=method)
+    return np.asarray(res.x, dtype=np.float64).tolist(), float(res.fun), bool(res.success)
+
+
+@pytest.mark.parametrize("size", [1, 2])
+def test_lbfgsb_docs_model_bounded_matches_scipy(size):
+    C.set_world_comm(None)
+    ref = _docs_bounded(0, 1, "scipy")
+    if size == 1:
+        res = [_docs_bounded(0, 1, "device")]
+    else:
+        res = run_distributed(_docs_bounded, size, "device")
+    for x, fun, ok in res:
+        assert ok
+        np.testing.assert_allclose(x, ref[0], atol=2e-4)
+        assert x[0] == pytest.approx(-1.95, abs=1e-7)   # on the bound, as scipy
+        assert fun == pytest.approx(ref[1], rel=1e-4)
+
+
+def _pop_lbfgsb(rank, size, zero, placement="hashed"):
+    comm = mg.get_world_comm()
+    data = make_population_data(num_params=80, num_halos=3000, seed=3, comm=comm, device="cpu",
+                                placement=placement)
+    m = PopulationSMFModel(aux_data=data, comm=comm)
+    m.set_target_from_truth()
+    g = data["guess"].cpu().numpy()
+    bounds = [(float(v) - 0.05, float(v) + 0.2) for v in g]
+    res = m.run_bfgs(data["guess"], maxsteps=30, method="device", zero=zero, chunks=3,
+                     param_bounds=bounds)
+    return res.x.numpy(), float(res.fun), int(res.nit), np.asarray(bounds)
+
+
+@pytest.mark.parametrize("placement", ["hashed", "owner"])
+def test_sharded_lbfgsb_matches_single_rank(placement):
+    """The engine-sharded L-BFGS-B (ZeRO slices / owner slices, breakpoints gathered
+    across ranks) against one rank."""
+    C.set_world_comm(None)
+    x1, f1, n1, b = _pop_lbfgsb(0, 1, False)
+    assert ((x1 >= b[:, 0] - 1e-6) & (x1 <= b[:, 1] + 1e-6)).all()
+    res = run_distributed(_pop_lbfgsb, 2, True, placement)
+    for x, f, nit, _ in res:
+        np.testing.assert_allclose(x, x1, rtol=1e-3, atol=2e-4)
+        assert f == pytest.approx(f1, rel=1e-2, abs=1e-9)
+    np.testing.assert_array_equal(res[0][0], res[1][0])
