@@ -149,7 +149,7 @@ class _History:
 
 def lbfgsb_minimize(obj, lo=None, hi=None, maxiter: int = 100, m: int = 10,
                     factr: float = 1e7, pgtol: float = 1e-5, maxls: int = 20,
-                    c1: float = 1e-4, c2: float = 0.9, K: int = 1024,
+                    c1: float = 1e-4, c2: float = 0.9, K: Optional[int] = None,
                     callback=None, gtol: Optional[float] = None,
                     ftol: Optional[float] = None) -> scipy.optimize.OptimizeResult:
     """Minimise ``obj`` subject to ``lo <= x <= hi`` (local slices of the optimizer's
@@ -194,21 +194,14 @@ def lbfgsb_minimize(obj, lo=None, hi=None, maxiter: int = 100, m: int = 10,
         pg = (torch.minimum(torch.maximum(x - g, lo), hi) - x).abs()
         vecs = [d] if pending is None else [H.s(pending), H.y(pending), d]
         dots_dev = dot(H.HS, 2 * R, vecs)
-        kk = min(K, n)
         tc = torch.where(free_path & torch.isfinite(t), t, torch.full_like(t, math.inf))
-        cand_t, cand_i = torch.topk(tc, kk, largest=False, sorted=False) if kk else \
-            (tc[:0], torch.zeros(0, dtype=torch.int64, device=dev))
-        cand = torch.cat([cand_t.reshape(1, -1), g[cand_i].reshape(1, -1),
-                          H.HS[:, cand_i]], 0).double()
         scal = torch.stack([(d.double() * d.double()).sum(),
                             pg.max().double() if n else torch.zeros((), dtype=torch.float64,
                                                                     device=dev),
                             torch.isfinite(tc).sum().double()])
-        packA = torch.cat([scal, dots_dev.reshape(-1), cand.reshape(-1)]).cpu().numpy()
+        packA = torch.cat([scal, dots_dev.reshape(-1)]).cpu().numpy()
         dd_l, pg_l, nfin_l = packA[:3]
-        nd = dots_dev.numel()
-        dots_l = packA[3:3 + nd].reshape(2 * R, len(vecs))
-        cand_l = packA[3 + nd:].reshape(2 + 2 * R, kk)
+        dots_l = packA[3:].reshape(2 * R, len(vecs))
         red = allsum(np.concatenate([[dd_l], dots_l.reshape(-1)]))
         dd, dots_np = red[0], red[1:].reshape(2 * R, len(vecs))
         pgmax = float(allmax([pg_l])[0])
@@ -223,25 +216,12 @@ def lbfgsb_minimize(obj, lo=None, hi=None, maxiter: int = 100, m: int = 10,
             break
         if k == maxiter:
             break
-        # breakpoints: the union of every rank's kk smallest is exact up to the smallest
-        # "largest gathered" value of the ranks that had more than kk
-        blocks = comm.allgather((cand_l, int(nfin_l))) if (sharded and comm is not None and
-                                                            comm.size > 1) else [(cand_l, int(nfin_l))]
-        t_cut = math.inf
-        for cb, nf in blocks:
-            if nf > cb.shape[1]:
-                t_cut = min(t_cut, float(cb[0].max()))
-        cand_all = np.concatenate([cb for cb, _ in blocks], 1)
-        cand_all = cand_all[:, cand_all[0] <= t_cut]
-        # ------------------------------------------------ generalized Cauchy point (host)
+        # ------------------------------------------------ generalized Cauchy point
         idx, M, WWt = H.compact()
         rows, fac = H.rows(idx)
         th = H.theta
-        tstar, cvec = _cauchy_scan(dd, Wd[rows] * fac, M, th, cand_all, rows, fac,
-                                   complete=not np.isfinite(t_cut))
-        if tstar is None:  # more breakpoints before the minimiser than gathered: grow K
-            K = 8 * K      # and redo this iteration's Cauchy point (state unchanged)
-            continue
+        tstar, cvec = _cauchy_point(dd, Wd[rows] * fac, M, th, tc, int(nfin_l), g, H.HS,
+                                    rows, fac, comm if sharded else None, K)
         xcp = torch.minimum(torch.maximum(x - tstar * g, lo), hi)
         free = (xcp > lo) & (xcp < hi)
         # ------------------------------------------------ copy B: subspace inner products
@@ -353,48 +333,108 @@ def lbfgsb_minimize(obj, lo=None, hi=None, maxiter: int = 100, m: int = 10,
         success=status == 0, message=message)
 
 
-def _cauchy_scan(dd, p, M, theta, cand, rows, fac, complete: bool):
-    """Segment scan of the projected-gradient path (Byrd et al. 1995, algorithm CP).
+def _cauchy_point(dd, p0, M, theta, tc, nfin, g, HS, rows, fac, comm, K):
+    """Generalized Cauchy point ``t*`` and ``c = W'(x^cp - x)`` (Byrd et al. 1995,
+    algorithm CP), over the breakpoints in increasing order, in batches.
 
-    ``p = W'd`` (2k), ``cand`` rows: [t, g, HS rows...] for breakpoints (any order).
-    Returns ``(t*, c)`` or ``(None, None)`` when the gathered breakpoints end before the
-    minimiser and more exist (``complete`` False)."""
-    fp = -dd
-    fpp = theta * dd - (p @ M @ p if p.size else 0.0)
-    c = np.zeros_like(p)
-    dtmin = -fp / fpp if fpp > 0 else math.inf
-    told = 0.0
-    order = np.argsort(cand[0], kind="stable")
-    Mp = M @ p if p.size else p
-    Mc = np.zeros_like(p)
-    broke = False
-    for j in order:
-        tb = cand[0, j]
-        if not np.isfinite(tb):
-            break
-        dt = tb - told
-        if dtmin < dt:
-            broke = True
-            break
-        gb = cand[1, j]
-        wb = cand[2 + rows, j] * fac if p.size else p
-        zb = -tb * gb
-        c = c + dt * p
-        Mc = Mc + dt * Mp
-        Mw = M @ wb if p.size else wb
-        fp = fp + dt * fpp + gb * gb + theta * gb * zb - (gb * (wb @ Mc) if p.size else 0.0)
-        fpp = fpp - theta * gb * gb - (2 * gb * (wb @ Mp) + gb * gb * (wb @ Mw) if p.size else 0.0)
-        p = p + gb * wb
-        Mp = Mp + gb * Mw
-        dtmin = -fp / fpp if fpp > 0 else math.inf
-        told = tb
-    if not broke and not complete:
-        return None, None
-    dtmin = max(dtmin, 0.0)
-    if not np.isfinite(dtmin):
-        dtmin = 0.0 if told > 0 else 1.0
-    c = c + dtmin * p
-    return told + dtmin, c
+    ``tc``: this rank's breakpoints (+inf where none), ``nfin`` of them finite.  Each batch
+    takes the next ``K`` of every rank (sorted on the device); across ranks the union is
+    exact up to the smallest "largest gathered" breakpoint of the ranks that have more,
+    and only that prefix is scanned (the rest waits for the next batch).  The scan of a
+    batch is vectorised: the running ``p``, ``c``, ``f'`` and ``f''`` of the sequential
+    algorithm are prefix sums over the sorted breakpoints (``_scan_batch``)."""
+    dev = tc.device
+    k2 = p0.size
+    Mt = torch.as_tensor(M, dtype=torch.float64, device=dev)
+    st = {"p": torch.as_tensor(p0, dtype=torch.float64, device=dev),
+          "c": torch.zeros(k2, dtype=torch.float64, device=dev),
+          "fp": -dd, "fpp": theta * dd - (float(p0 @ M @ p0) if k2 else 0.0), "told": 0.0}
+    order = torch.argsort(tc)
+    rows_t = torch.as_tensor(rows, dtype=torch.int64, device=dev)
+    fac_t = torch.as_tensor(fac, dtype=torch.float64, device=dev)
+    multi = comm is not None and comm.size > 1
+    B = int(K) if K is not None else (1 << 16 if multi else 1 << 20)
+    ptr = 0
+    while True:
+        sel = order[ptr:ptr + B]
+        tb = tc[sel].double()
+        gb = g[sel].double()
+        Wb = (HS[rows_t][:, sel].double().T * fac_t) if k2 else \
+            torch.zeros((sel.numel(), 0), dtype=torch.float64, device=dev)
+        left = nfin - ptr  # this rank's finite breakpoints not yet scanned
+        if multi:
+            rec = torch.full((B, 2 + k2), math.inf, dtype=torch.float64, device=dev)
+            nb = sel.numel()
+            rec[:nb, 0], rec[:nb, 1], rec[:nb, 2:] = tb, gb, Wb
+            rec[nb:, 1:] = 0.0
+            hdr = torch.tensor([[float(left)] + [0.0] * (1 + k2)], dtype=torch.float64, device=dev)
+            mine = torch.cat([hdr, rec]).contiguous()
+            allr = torch.empty((comm.size,) + tuple(mine.shape), dtype=torch.float64, device=dev)
+            comm.all_gather_into_tensor(allr.reshape(-1), mine.reshape(-1))
+            lefts = allr[:, 0, 0].cpu().numpy()
+            t_cut = math.inf
+            for r in range(comm.size):
+                if lefts[r] > B:
+                    t_cut = min(t_cut, float(allr[r, 1 + B - 1, 0]))
+            recs = allr[:, 1:].reshape(-1, 2 + k2)
+            keep = recs[:, 0] <= t_cut
+            recs = recs[keep & torch.isfinite(recs[:, 0])]
+            recs = recs[torch.argsort(recs[:, 0], stable=True)]
+            tb, gb, Wb = recs[:, 0], recs[:, 1], recs[:, 2:]
+            mine_used = int(((rec[:, 0] <= t_cut) & torch.isfinite(rec[:, 0])).sum().item())
+            more = bool((lefts > B).any())
+        else:
+            fin = torch.isfinite(tb)
+            tb, gb, Wb = tb[fin], gb[fin], Wb[fin]
+            mine_used = sel.numel()
+            more = left > B
+        found, tstar, c = _scan_batch(st, tb, gb, Wb, Mt, theta)
+        if found:
+            return tstar, c.cpu().numpy()
+        ptr += mine_used
+        if not more:
+            dtmin = -st["fp"] / st["fpp"] if st["fpp"] > 0 else 0.0
+            dtmin = max(dtmin, 0.0)
+            c = st["c"] + dtmin * st["p"]
+            return st["told"] + dtmin, c.cpu().numpy()
+
+
+def _scan_batch(st, t, g, W, M, theta):
+    """One batch of the Cauchy-point scan (sorted breakpoints ``t``, gradient entries
+    ``g``, rows ``W`` of ``[Y, theta S]``).  Returns ``(True, t*, c)`` when the minimiser
+    lies in a segment of this batch, else advances ``st`` past it and returns ``(False,
+    None, None)``."""
+    N = t.numel()
+    if N == 0:
+        return False, None, None
+    told0 = st["told"]
+    prev = torch.cat([torch.tensor([told0], dtype=torch.float64, device=t.device), t[:-1]])
+    dt = t - prev
+    gw = g[:, None] * W
+    P = st["p"][None, :] + torch.cumsum(gw, 0) - gw          # p before breakpoint i
+    Mw = W @ M                                               # (M w_i)' (M symmetric)
+    wMp = (Mw * P).sum(1)
+    wMw = (Mw * W).sum(1)
+    dfpp = -theta * g * g - 2 * g * wMp - g * g * wMw
+    fpp_b = st["fpp"] + torch.cumsum(dfpp, 0) - dfpp          # f'' at the start of segment i
+    Cp = st["c"][None, :] + torch.cumsum(dt[:, None] * P, 0)  # c after breakpoint i
+    wMc = (Mw * Cp).sum(1)
+    dfp = dt * fpp_b + g * g - theta * t * g * g - g * wMc
+    fp_b = st["fp"] + torch.cumsum(dfp, 0) - dfp              # f' at the start of segment i
+    dtmin = torch.where(fpp_b > 0, -fp_b / fpp_b, torch.full_like(fp_b, math.inf))
+    stop = dtmin < dt
+    if bool(stop.any().item()):
+        j = int(torch.nonzero(stop)[0, 0].item())
+        told = float(prev[j].item())
+        dtm = max(float(dtmin[j].item()), 0.0)
+        c_prev = Cp[j - 1] if j > 0 else st["c"]
+        return True, told + dtm, c_prev + dtm * P[j]
+    st["p"] = P[-1] + gw[-1]
+    st["c"] = Cp[-1]
+    st["fp"] = float((fp_b[-1] + dfp[-1]).item())
+    st["fpp"] = float((fpp_b[-1] + dfpp[-1]).item())
+    st["told"] = float(t[-1].item())
+    return False, None, None
 
 
 def _line_search(phi, f0, d0_box, a1, c1, c2, maxls):

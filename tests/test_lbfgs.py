@@ -160,9 +160,9 @@ def test_lbfgsb_matches_scipy_on_bounded_1e4_problem():
     assert abs(res.nit - ref.nit) <= 5
 
 
-def test_lbfgsb_small_breakpoint_budget_grows():
-    """A gathered-breakpoint budget far below the number of breakpoints on the path
-    (K=4) must give the same result (the scan asks for more)."""
+def test_lbfgsb_small_breakpoint_batches():
+    """Breakpoint batches far smaller than the number of breakpoints before the Cauchy
+    point (K=4: the scan carries its state across ~100 batches) give the same result."""
     n = 300
     lo, hi, f_np, lg = _bounded_problem(n, seed=2)
     x0 = torch.tensor(np.clip(np.zeros(n), lo, hi), dtype=torch.float32)
@@ -172,6 +172,7 @@ def test_lbfgsb_small_breakpoint_budget_grows():
     b = LB.lbfgsb_minimize(obj, torch.tensor(lo, dtype=torch.float32),
                            torch.tensor(hi, dtype=torch.float32), maxiter=200)
     assert a.fun == pytest.approx(b.fun, rel=1e-7)
+    np.testing.assert_allclose(a.x.numpy(), b.x.numpy(), atol=1e-6)
 
 
 def _docs_bounded(rank, size, method):
@@ -196,6 +197,52 @@ def test_lbfgsb_docs_model_bounded_matches_scipy(size):
         np.testing.assert_allclose(x, ref[0], atol=2e-4)
         assert x[0] == pytest.approx(-1.95, abs=1e-7)   # on the bound, as scipy
         assert fun == pytest.approx(ref[1], rel=1e-4)
+
+
+def test_cauchy_scan_vectorised_matches_sequential():
+    """The prefix-sum Cauchy-point scan against the sequential algorithm CP of Byrd et al.
+    (1995), with a non-trivial compact matrix and many breakpoints, in batches."""
+    import math
+    rng = np.random.default_rng(3)
+    n, k = 400, 3
+    S = rng.normal(size=(k, n))
+    Y = S + 0.2 * rng.normal(size=(k, n))
+    theta = float((Y[-1] @ Y[-1]) / (S[-1] @ Y[-1]))
+    sy = S @ Y.T
+    D = np.diag(np.diag(sy))
+    Lm = np.tril(sy, -1)
+    M = np.linalg.inv(np.block([[-D, Lm.T], [Lm, theta * (S @ S.T)]]))
+    Wrows = np.concatenate([Y, theta * S])          # rows of W' (2k x n)
+    g = rng.normal(size=n)
+    t = np.where(rng.random(n) < 0.7, rng.random(n) * 3, np.inf)
+    d = np.where(t > 0, -g, 0.0)
+    dd = float(d @ d)
+    p0 = Wrows @ d
+    # sequential reference
+    fp, fpp = -dd, theta * dd - p0 @ M @ p0
+    p, c, told = p0.copy(), np.zeros(2 * k), 0.0
+    dtmin = -fp / fpp
+    for j in np.argsort(t):
+        if not np.isfinite(t[j]) or dtmin < t[j] - told:
+            break
+        dt, gb, wb = t[j] - told, g[j], Wrows[:, j]
+        c = c + dt * p
+        fp = fp + dt * fpp + gb * gb - theta * t[j] * gb * gb - gb * (wb @ M @ c)
+        fpp = fpp - theta * gb * gb - 2 * gb * (wb @ M @ p) - gb * gb * (wb @ M @ wb)
+        p = p + gb * wb
+        dtmin = -fp / fpp
+        told = t[j]
+    dtmin = max(dtmin, 0.0)
+    want_t, want_c = told + dtmin, c + dtmin * p
+    HS = torch.tensor(np.concatenate([S, Y]), dtype=torch.float32)  # rows s_0..s_k-1, y_0..
+    rows = np.concatenate([k + np.arange(k), np.arange(k)])
+    fac = np.concatenate([np.ones(k), np.full(k, theta)])
+    HSd = torch.tensor(np.concatenate([S, Y]), dtype=torch.float64)
+    for K in (3, 50, 10_000):
+        ts, cs = LB._cauchy_point(dd, p0, M, theta, torch.tensor(t), int(np.isfinite(t).sum()),
+                                  torch.tensor(g), HSd, rows, fac, None, K)
+        assert ts == pytest.approx(want_t, rel=1e-10)
+        np.testing.assert_allclose(cs, want_c, rtol=1e-9, atol=1e-12)
 
 
 def _pop_lbfgsb(rank, size, zero, placement="hashed"):

@@ -63,8 +63,10 @@ def test_zero_engine_schedule_over_rccl():
 
 
 def test_onepoint_group_on_rccl_subcommunicators(monkeypatch):
-    """OnePointGroup with each model on its own RCCL communicator and the group sum over a
-    third one (device all-reduces through RCCL, 1 rank each)."""
+    """OnePointGroup with each model on its own RCCL-backed communicator and the group sum
+    over a third one, on the GPU (1 rank each: the communicators short-circuit their
+    collectives at size 1, so this pins the group plumbing on device tensors; the
+    multi-rank sums are covered on gloo by test_models.py)."""
     monkeypatch.setenv("MULTIGRAD_ALLREDUCE", "rccl")
     import multigrad_amd as mg
     from multigrad_amd.models.smf import DocsSMFModel, make_docs_data
@@ -80,6 +82,6 @@ def test_onepoint_group_on_rccl_subcommunicators(monkeypatch):
     lb, gb = mb.calc_loss_and_grad_from_params(p)
     torch.testing.assert_close(loss, la + lb)
     torch.testing.assert_close(grad, ga + gb)
-    assert main._dev is not None and sub_a._dev is not None
+    assert grad.is_cuda and loss.is_cuda
     res = grp.run_bfgs(p, maxsteps=30)
     assert res.success or res.nit > 0
