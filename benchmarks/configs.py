@@ -12,6 +12,8 @@
     python -m multigrad_amd.launch -n 8 benchmarks/configs.py --which adam1e6 lbfgs adam1e8
 """
 import argparse
+
+import numpy as np
 import json
 import os
 import sys
@@ -101,17 +103,18 @@ def lbfgsb(comm, iters, params, halos):
     m = PopulationSMFModel(aux_data=data, comm=comm)
     m.set_target_from_truth()
     g = data["guess"].detach().cpu().numpy()
-    bounds = list(zip((g - 0.15).tolist(), (g + 0.05).tolist()))
+    bounds = np.stack([g - 0.15, g + 0.05], 1)  # (P, 2) array: the truth (g - 0.1) inside
 
-    def run(n):
+    def prep():
         obj = m.fused_engine().lbfgs_objective(data["guess"])
-        lo, hi = obj.local_box(bounds)
-        return obj, lbfgsb_minimize(obj, lo, hi, maxiter=n, pgtol=0.0, factr=0.0)
+        return (obj,) + tuple(obj.local_box(bounds))
 
-    run(2)  # warm-up (kernel loading)
+    obj, lo, hi = prep()
+    lbfgsb_minimize(obj, lo, hi, maxiter=2, pgtol=0.0, factr=0.0)  # warm-up (kernel loading)
+    obj, lo, hi = prep()
     _sync(); comm.barrier()
     t0 = time.perf_counter()
-    obj, res = run(iters)
+    res = lbfgsb_minimize(obj, lo, hi, maxiter=iters, pgtol=0.0, factr=0.0)
     _sync(); comm.barrier()
     dt = time.perf_counter() - t0
     return {"config": f"lbfgsb-{params:.0e}param", "value": res.nit / dt, "unit": "iterations/s",

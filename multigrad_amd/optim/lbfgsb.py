@@ -191,7 +191,8 @@ def lbfgsb_minimize(obj, lo=None, hi=None, maxiter: int = 100, m: int = 10,
         t = torch.where(torch.isnan(t), torch.full_like(t, math.inf), t)
         free_path = t > 0
         d = torch.where(free_path, -g, torch.zeros_like(g))
-        pg = (torch.minimum(torch.maximum(x - g, lo), hi) - x).abs()
+        xd = x.double()
+        pg = (torch.minimum(torch.maximum(xd - g.double(), lo.double()), hi.double()) - xd).abs()
         vecs = [d] if pending is None else [H.s(pending), H.y(pending), d]
         dots_dev = dot(H.HS, 2 * R, vecs)
         tc = torch.where(free_path & torch.isfinite(t), t, torch.full_like(t, math.inf))
@@ -359,13 +360,13 @@ def _cauchy_point(dd, p0, M, theta, tc, nfin, g, HS, rows, fac, comm, K):
         sel = order[ptr:ptr + B]
         tb = tc[sel].double()
         gb = g[sel].double()
-        Wb = (HS[rows_t][:, sel].double().T * fac_t) if k2 else \
-            torch.zeros((sel.numel(), 0), dtype=torch.float64, device=dev)
+        Wb = (HS[rows_t][:, sel].double() * fac_t[:, None]) if k2 else \
+            torch.zeros((0, sel.numel()), dtype=torch.float64, device=dev)
         left = nfin - ptr  # this rank's finite breakpoints not yet scanned
         if multi:
             rec = torch.full((B, 2 + k2), math.inf, dtype=torch.float64, device=dev)
             nb = sel.numel()
-            rec[:nb, 0], rec[:nb, 1], rec[:nb, 2:] = tb, gb, Wb
+            rec[:nb, 0], rec[:nb, 1], rec[:nb, 2:] = tb, gb, Wb.T
             rec[nb:, 1:] = 0.0
             hdr = torch.tensor([[float(left)] + [0.0] * (1 + k2)], dtype=torch.float64, device=dev)
             mine = torch.cat([hdr, rec]).contiguous()
@@ -380,12 +381,12 @@ def _cauchy_point(dd, p0, M, theta, tc, nfin, g, HS, rows, fac, comm, K):
             keep = recs[:, 0] <= t_cut
             recs = recs[keep & torch.isfinite(recs[:, 0])]
             recs = recs[torch.argsort(recs[:, 0], stable=True)]
-            tb, gb, Wb = recs[:, 0], recs[:, 1], recs[:, 2:]
+            tb, gb, Wb = recs[:, 0], recs[:, 1], recs[:, 2:].T.contiguous()
             mine_used = int(((rec[:, 0] <= t_cut) & torch.isfinite(rec[:, 0])).sum().item())
             more = bool((lefts > B).any())
         else:
             fin = torch.isfinite(tb)
-            tb, gb, Wb = tb[fin], gb[fin], Wb[fin]
+            tb, gb, Wb = tb[fin], gb[fin], Wb[:, fin]
             mine_used = sel.numel()
             more = left > B
         found, tstar, c = _scan_batch(st, tb, gb, Wb, Mt, theta)
@@ -401,39 +402,42 @@ def _cauchy_point(dd, p0, M, theta, tc, nfin, g, HS, rows, fac, comm, K):
 
 def _scan_batch(st, t, g, W, M, theta):
     """One batch of the Cauchy-point scan (sorted breakpoints ``t``, gradient entries
-    ``g``, rows ``W`` of ``[Y, theta S]``).  Returns ``(True, t*, c)`` when the minimiser
-    lies in a segment of this batch, else advances ``st`` past it and returns ``(False,
-    None, None)``."""
+    ``g``, columns ``W`` (2k x N) = rows of ``[Y, theta S]`` at the breakpoints).  Returns
+    ``(True, t*, c)`` when the minimiser lies in a segment of this batch, else advances
+    ``st`` past it and returns ``(False, None, None)``.  The 2k-vectors are kept as
+    (2k x N) so every prefix sum runs along the contiguous dimension."""
     N = t.numel()
     if N == 0:
         return False, None, None
     told0 = st["told"]
-    prev = torch.cat([torch.tensor([told0], dtype=torch.float64, device=t.device), t[:-1]])
+    prev = torch.cat([torch.full((1,), told0, dtype=torch.float64, device=t.device), t[:-1]])
     dt = t - prev
-    gw = g[:, None] * W
-    P = st["p"][None, :] + torch.cumsum(gw, 0) - gw          # p before breakpoint i
-    Mw = W @ M                                               # (M w_i)' (M symmetric)
-    wMp = (Mw * P).sum(1)
-    wMw = (Mw * W).sum(1)
+    gw = W * g[None, :]
+    P = st["p"][:, None] + torch.cumsum(gw, 1) - gw          # p before breakpoint i
+    Mw = M @ W                                               # M w_i (M symmetric)
+    wMp = (Mw * P).sum(0)
+    wMw = (Mw * W).sum(0)
     dfpp = -theta * g * g - 2 * g * wMp - g * g * wMw
     fpp_b = st["fpp"] + torch.cumsum(dfpp, 0) - dfpp          # f'' at the start of segment i
-    Cp = st["c"][None, :] + torch.cumsum(dt[:, None] * P, 0)  # c after breakpoint i
-    wMc = (Mw * Cp).sum(1)
+    Cp = st["c"][:, None] + torch.cumsum(P * dt[None, :], 1)  # c after breakpoint i
+    wMc = (Mw * Cp).sum(0)
     dfp = dt * fpp_b + g * g - theta * t * g * g - g * wMc
     fp_b = st["fp"] + torch.cumsum(dfp, 0) - dfp              # f' at the start of segment i
     dtmin = torch.where(fpp_b > 0, -fp_b / fpp_b, torch.full_like(fp_b, math.inf))
     stop = dtmin < dt
-    if bool(stop.any().item()):
-        j = int(torch.nonzero(stop)[0, 0].item())
-        told = float(prev[j].item())
+    # one host copy: the first stop index (or -1) and the end-of-batch state
+    first = torch.where(stop.any(), torch.argmax(stop.to(torch.int8)).to(torch.float64),
+                        torch.full((), -1.0, dtype=torch.float64, device=t.device))
+    tail = torch.stack([first, fp_b[-1] + dfp[-1], fpp_b[-1] + dfpp[-1], t[-1]]).cpu().numpy()
+    j = int(tail[0])
+    if j >= 0:
+        told = told0 if j == 0 else float(t[j - 1].item())
         dtm = max(float(dtmin[j].item()), 0.0)
-        c_prev = Cp[j - 1] if j > 0 else st["c"]
-        return True, told + dtm, c_prev + dtm * P[j]
-    st["p"] = P[-1] + gw[-1]
-    st["c"] = Cp[-1]
-    st["fp"] = float((fp_b[-1] + dfp[-1]).item())
-    st["fpp"] = float((fpp_b[-1] + dfpp[-1]).item())
-    st["told"] = float(t[-1].item())
+        c_prev = Cp[:, j - 1] if j > 0 else st["c"]
+        return True, told + dtm, c_prev + dtm * P[:, j]
+    st["p"] = P[:, -1] + gw[:, -1]
+    st["c"] = Cp[:, -1]
+    st["fp"], st["fpp"], st["told"] = float(tail[1]), float(tail[2]), float(tail[3])
     return False, None, None
 
 
@@ -479,6 +483,11 @@ def bounds_arrays(param_bounds, n: int):
     ``(ndim, 2)`` with ``None`` entries, or ``(None, None)``."""
     if param_bounds is None:
         return None, None
+    if isinstance(param_bounds, (np.ndarray, torch.Tensor)):
+        b = np.asarray(param_bounds.detach().cpu() if isinstance(param_bounds, torch.Tensor)
+                       else param_bounds, dtype=np.float64).reshape(n, 2)
+        b = np.where(np.isnan(b), np.array([-np.inf, np.inf]), b)
+        return b[:, 0].astype(np.float32), b[:, 1].astype(np.float32)
     lo = np.full(n, -np.inf)
     hi = np.full(n, np.inf)
     for i, b in enumerate(param_bounds):
