@@ -1,0 +1,52 @@
+"""Generic-model Adam on one MI355X: the population SMF model written in plain torch ops
+(``models/torch_population.py``): eager distributed chain rule + run_adam (a Python loop
+of torch launches), the generic engine forced to replay one HIP graph per step, and the
+default front-end path (the generic engine's auto policy).  One JSON line per path."""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+os.environ.setdefault("MULTIGRAD_PROGRESS", "0")
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__)
+    ap.add_argument("--params", type=int, default=1_000_000)
+    ap.add_argument("--halos", type=int, default=10_000_000)
+    ap.add_argument("--steps", type=int, default=30)
+    a = ap.parse_args(argv)
+    from multigrad_amd.engine.generic import GraphAdamEngine
+    from multigrad_amd.models.population import PopulationSMFModel, make_population_data
+    from multigrad_amd.models.torch_population import TorchPopulationSMFModel, torch_population_data
+    dev = torch.device("cuda", 0)
+    data = make_population_data(a.params, a.halos, seed=5, device=dev)
+    PopulationSMFModel(aux_data=data).set_target_from_truth()
+    m = TorchPopulationSMFModel(aux_data=torch_population_data(data))
+    guess = data["guess"]
+    out = {}
+    for name, fn in (("eager", lambda n: m.run_adam(guess, nsteps=n, learning_rate=1e-3,
+                                                    use_engine=False)),
+                     ("graph", lambda n: GraphAdamEngine(m, graph=True).run_adam(
+                         guess, nsteps=n, learning_rate=1e-3)),
+                     ("auto", lambda n: m.run_adam(guess, nsteps=n, learning_rate=1e-3))):
+        fn(3)  # warm-up (kernel loading, capture)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        traj = fn(a.steps)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        out[name] = a.steps / dt
+        print(json.dumps({"config": f"generic-torch-population-{a.params:.0e}param", "path": name,
+                          "steps_per_s": round(a.steps / dt, 2), "halos": a.halos,
+                          "final_param_0": float(traj[-1, 0])}), flush=True)
+    print(json.dumps({"graph_speedup": round(out["graph"] / out["eager"], 3),
+                      "auto_speedup": round(out["auto"] / out["eager"], 3)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

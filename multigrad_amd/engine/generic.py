@@ -1,0 +1,342 @@
+"""Graph-captured Adam engine for ANY torch ``OnePointModel``.
+
+The reference's distributed chain rule works for every user model
+(multigrad/multigrad.py:508-538) and its Adam loop is ``jax.example_libraries`` Adam
+driven from Python (multigrad/adam.py:52-68).  The eager equivalent here
+(``OnePointModel._vjp`` + :func:`multigrad_amd.optim.adam.run_adam`) launches every torch
+op of the user's hooks from Python each step.  This engine instead records ONE optimizer
+step of a user model -- its autograd forward, the sumstat all-reduce, the loss cotangent,
+the VJP, the dense-gradient sum and the fused Adam update with the trajectory write --
+into a HIP graph, and replays it:
+
+    partial = calc_partial_sumstats_from_params(p)          # user hook, autograd
+    S = sum_ranks(partial)       one-shot xGMI kernel (<= 64 floats) | RCCL
+    cot = d loss(S) / dS                                    # user hook, autograd
+    g = VJP(partial, p, cot)
+    world 1:  fused Adam (bounded or not) + trajectory row  (csrc/adam.hip)
+    world W:  two-shot kernel: reduce-scatter g -> Adam on the owned 1/W -> all-gather p
+              (csrc/xgmi.hip), or RCCL all-reduce + fused Adam
+
+A step is replayable only if every collective in it is a peer-memory kernel with its
+sequence number on the device (one rank, or one-shot + two-shot) and the user hooks make
+no host synchronisation; the step counter lives on the device so replays self-advance.
+Anything else -- RCCL collectives, a capture error in user code, per-step PRNG keys --
+runs the same step eagerly (the reason is kept in ``fallback_reason``).  By default the
+engine times a few eager steps against a few replays and keeps the faster mode
+(``tuning``): replays remove the per-op launch cost but measured slower than eager
+launches once the step is GPU bound.
+
+The gradient exchange is one bucket after the VJP: a generic model consumes its
+parameters as one tensor, so autograd produces the whole gradient at once and there is
+nothing to overlap inside the VJP.
+"""
+from __future__ import annotations
+
+import math
+import os
+from typing import Optional
+
+import torch
+
+from ..ops.adam import adam_step_
+from ..optim.adam import History
+from ..optim.transforms import Bounds
+from ..utils.tensors import as_param_tensor
+
+__all__ = ["GraphAdamEngine"]
+
+
+class GraphAdamEngine:
+    """Adam over a generic :class:`~multigrad_amd.models.onepoint.OnePointModel`.
+
+    ``graph``: None (default) = capture when the step is capturable; False = eager;
+    True = capture or raise.  ``MULTIGRAD_GRAPH`` overrides None."""
+
+    def __init__(self, model, comm=None, graph: Optional[bool] = None):
+        self.model = model
+        self.comm = model.comm if comm is None else comm
+        self.size = 1 if self.comm is None else self.comm.size
+        self.rank = 0 if self.comm is None else self.comm.rank
+        env = os.environ.get("MULTIGRAD_GRAPH")
+        if graph is None and env is not None:
+            graph = env.lower() not in ("0", "false", "off", "no")
+        self.graph_req = graph
+        self.graph = None
+        self.use_graph = False
+        self.fallback_reason = None
+        self.oneshot = None
+        self.twoshot = None
+
+    # ------------------------------------------------------------------ setup
+    def setup(self, guess, nsteps: int, param_bounds=None, learning_rate: float = 0.01,
+              b1: float = 0.9, b2: float = 0.999, eps: float = 1e-8, history="full",
+              legacy_bounds_jacobian: bool = False):
+        md = self.model
+        p0 = as_param_tensor(guess, device=md.param_device()).detach()
+        self.shape = tuple(p0.shape)
+        p0 = p0.reshape(-1).to(torch.float32)
+        dev = p0.device
+        self.device = dev
+        self.P = P = p0.numel()
+        W = self.size
+        self.lr, self.b1, self.b2, self.eps = float(learning_rate), float(b1), float(b2), float(eps)
+        self.legacy = bool(legacy_bounds_jacobian)
+        bounds = Bounds.from_spec(param_bounds, P, device=dev)
+        cuda = dev.type == "cuda"
+        if cuda and W > 1:
+            from ..parallel.xgmi import connect_twoshot, get_oneshot, twoshot_enabled
+            q = 4 * W
+            P_pad = -(-P // q) * q
+            self.twoshot = connect_twoshot(self.comm, P_pad) if twoshot_enabled() else None
+            self.oneshot = get_oneshot(self.comm)
+        else:
+            P_pad = P
+        self.P_pad = P_pad if self.twoshot is not None else P
+        f32 = dict(dtype=torch.float32, device=dev)
+        if self.twoshot is not None:
+            self.p = self.twoshot.theta
+            self.p.zero_()
+            self.gbuf = self.twoshot.grad
+            self.gbuf.zero_()
+        else:
+            self.p = torch.zeros(self.P_pad, **f32)
+            self.gbuf = None
+        start = bounds.inverse(bounds.forward(p0)) if bounds is not None else p0
+        self.p[:P].copy_(start)
+        if bounds is not None and self.P_pad > P:
+            pad = self.P_pad - P
+            bounds = Bounds(torch.cat([bounds.lo, torch.full((pad,), -math.inf, **f32)]),
+                            torch.cat([bounds.hi, torch.full((pad,), math.inf, **f32)]),
+                            torch.cat([bounds.kind, torch.zeros(pad, dtype=torch.int8, device=dev)]))
+        self.bounds = bounds
+        if self.twoshot is not None:
+            lo_, n_ = self.twoshot.slice()
+            self.own = (lo_, lo_ + n_)
+            self.m = torch.zeros(n_, **f32)
+            self.v = torch.zeros(n_, **f32)
+            self.bounds_loc = None if bounds is None else Bounds(
+                bounds.lo[lo_:lo_ + n_].contiguous(), bounds.hi[lo_:lo_ + n_].contiguous(),
+                bounds.kind[lo_:lo_ + n_].contiguous())
+            self.u = None if bounds is None else self.bounds_loc.forward(self.p[lo_:lo_ + n_]).contiguous()
+        else:
+            self.own = (0, self.P_pad)
+            self.m = torch.zeros(self.P_pad, **f32)
+            self.v = torch.zeros(self.P_pad, **f32)
+            self.bounds_loc = bounds
+            self.u = bounds.forward(self.p).contiguous() if bounds is not None else self.p
+        self.step_dev = torch.zeros(2, dtype=torch.int32, device=dev)
+        self.loss = torch.zeros(1, **f32)
+        self.nsteps = int(nsteps)
+        self.step_host = 0
+        self.history_mode = history
+        if self.twoshot is not None and history == "full":
+            a, b = self.own
+            self.traj_loc = torch.zeros((self.nsteps + 1, b - a), **f32)
+            self.traj_loc[0] = self.p[a:b]
+            self.history = History("last", nsteps, self.p[:P].clone())
+        else:
+            self.traj_loc = None
+            self.history = History(history, nsteps, self.p[:P].clone())
+        self.graph = None
+        self.tuning = None
+        self._times = {"eager": [], "graph": []}
+        capturable = cuda and (W == 1 or (self.twoshot is not None and self.oneshot is not None))
+        if self.graph_req is True and not capturable:
+            raise RuntimeError("this step is not capturable (RCCL collectives in it)")
+        self.use_graph = capturable and self.graph_req is not False
+        if not capturable and self.graph_req is None:
+            self.fallback_reason = "RCCL / gloo collectives in the step" if W > 1 else \
+                "CPU tensors"
+        self.ready = True
+        return self
+
+    # ------------------------------------------------------------------ the step
+    def _sumstats_allreduce(self, S: torch.Tensor) -> torch.Tensor:
+        if self.size == 1:
+            return S
+        S = S.contiguous()
+        if self.oneshot is not None and S.dtype == torch.float32 and S.numel() <= 64:
+            self.oneshot(S)
+            return S
+        self.comm.all_reduce(S)
+        return S
+
+    def _body(self, host_step: Optional[int]):
+        md, P = self.model, self.P
+        with torch.enable_grad():
+            leaf = self.p[:P].detach().view(self.shape).requires_grad_(True)
+            partial = torch.as_tensor(md.calc_partial_sumstats_from_params(leaf))
+            if md.sumstats_func_has_aux:
+                raise TypeError("the graph engine needs sumstats without aux")
+            total = self._sumstats_allreduce(partial.detach().clone())
+            total = total.to(partial.dtype).requires_grad_(True)
+            out = md.calc_loss_from_sumstats(total)
+            loss = out[0] if md.loss_func_has_aux else out
+            (cot,) = torch.autograd.grad(loss, total, allow_unused=True)
+            if cot is None:
+                cot = torch.zeros_like(total)
+            (g,) = torch.autograd.grad(partial, leaf, cot, allow_unused=True)
+        self.loss.copy_(loss.detach().reshape(1).to(torch.float32))
+        g = torch.zeros(self.shape, device=self.device) if g is None else g
+        g = g.reshape(-1).to(torch.float32)
+        hb = self.history.buf.reshape(-1) if self.history.mode == "full" else None
+        if self.twoshot is not None:
+            self.gbuf[:P].copy_(g)
+            a, b = self.own
+            bnd = self.bounds_loc
+            mode = 1 if bnd is None else (3 if self.legacy else 2)
+            traj = None if self.traj_loc is None else self.traj_loc.reshape(-1)
+            self.twoshot.step(a, b - a, mode, m=self.m, v=self.v, u=self.u, bounds=bnd,
+                              traj=traj, traj_stride=0 if traj is None else b - a,
+                              step=self.step_dev, host_step=host_step, lr=self.lr, b1=self.b1,
+                              b2=self.b2, eps=self.eps)
+            return
+        if self.size > 1:
+            g = g.contiguous()
+            self.comm.all_reduce(g)
+        bnd = self.bounds
+        adam_step_(self.u, self.m, self.v, g, self.p if bnd is not None else None,
+                   self.step_dev, self.lr, self.b1, self.b2, self.eps, bnd, self.legacy,
+                   traj_base=hb, traj_stride=P if hb is not None else 0, host_step=host_step)
+
+    def _capture(self):
+        """Warm up on a side stream (allocator, autograd and kernel loading), restore the
+        state the warm-up moved, then capture one step.  Collectives in the warm-up run on
+        every rank alike, so their device sequence numbers stay in lockstep."""
+        saved = [t.clone() for t in (self.p, self.m, self.v, self.step_dev)]
+        u_saved = self.u.clone() if self.u is not None and self.u is not self.p else None
+        traj_saved = None if self.traj_loc is None else self.traj_loc[1].clone()
+        hist_saved = None if self.history.mode != "full" else self.history.buf[1].clone()
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            self._body(None)  # one warm-up step (it writes trajectory row 1, restored below)
+        torch.cuda.current_stream().wait_stream(s)
+        for t, v in zip((self.p, self.m, self.v, self.step_dev), saved):
+            t.copy_(v)
+        if u_saved is not None:
+            self.u.copy_(u_saved)
+        if traj_saved is not None:
+            self.traj_loc[1].copy_(traj_saved)
+        if hist_saved is not None:
+            self.history.buf[1].copy_(hist_saved)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            self._body(None)
+        return graph
+
+    _TUNE = 3  # steps timed per mode by the auto policy
+
+    def _tuned_step(self):
+        """Auto policy (``graph=None``): the first steps run eagerly, the next ones from
+        the captured graph, each timed; the faster mode is kept (a collective decision).
+        Graph replay wins when the step is launch bound (1.8x on a 1e4-parameter torch
+        model) and loses ~10% when it is GPU bound (1e6 parameters): both measured on
+        one MI355X (profiles/generic_engine.md)."""
+        import time
+        k = self.step_host
+        mode = "eager" if k < self._TUNE else "graph"
+        if mode == "graph" and self.graph is None:
+            self.step_dev[0] = k   # eager steps keep the count on the host
+            try:
+                self.graph = self._capture()
+            except Exception as exc:  # noqa: BLE001
+                if self.size > 1:
+                    raise
+                torch.cuda.synchronize()
+                self.use_graph = False
+                self.fallback_reason = f"capture failed: {type(exc).__name__}: {exc}"
+                self._body(k)
+                return
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        if mode == "graph":
+            self.graph.replay()
+        else:
+            self._body(k)
+        torch.cuda.synchronize()
+        self._times[mode].append(time.perf_counter() - t0)
+        if mode == "graph" and len(self._times["graph"]) == self._TUNE:
+            te, tg = min(self._times["eager"]), min(self._times["graph"])
+            keep = 1 if tg < te else 0
+            if self.size > 1:
+                keep = int(all(self.comm.allgather(keep)))
+            self.tuning = {"eager_s": te, "graph_s": tg, "graph": bool(keep)}
+            if not keep:
+                self.use_graph = False
+                self.graph = None
+                self.fallback_reason = f"eager measured faster ({te * 1e3:.3f} vs {tg * 1e3:.3f} ms/step)"
+
+    def step(self):
+        assert self.ready, "call setup() first"
+        if self.step_host >= self.nsteps and (self.history.mode == "full" or self.traj_loc is not None):
+            raise RuntimeError("more steps than the trajectory buffer was sized for")
+        if self.use_graph and self.graph_req is None and self.tuning is None and \
+                self.nsteps > 2 * self._TUNE:
+            self._tuned_step()
+            self.step_host += 1
+            if self.history.mode != "full" and self.traj_loc is None:
+                self.history.record(self.step_host - 1, self.p[:self.P])
+            return
+        if self.use_graph and self.graph is None:
+            try:
+                self.graph = self._capture()
+            except Exception as exc:  # noqa: BLE001  (host sync / dynamic shapes in user code)
+                if self.graph_req is True or self.size > 1:
+                    raise
+                torch.cuda.synchronize()
+                self.use_graph = False
+                self.fallback_reason = f"capture failed: {type(exc).__name__}: {exc}"
+        if self.use_graph:
+            self.graph.replay()
+        else:
+            self._body(self.step_host)
+        self.step_host += 1
+        if self.history.mode != "full" and self.traj_loc is None:
+            self.history.record(self.step_host - 1, self.p[:self.P])
+
+    # ------------------------------------------------------------------ results
+    def check(self, where: str = "", collective: bool = False) -> None:
+        comm = self.comm if collective else None
+        for ctx in (self.twoshot, self.oneshot):
+            if ctx is not None:
+                ctx.check(where or f"generic engine step {self.step_host}", comm=comm)
+
+    def last_loss(self) -> float:
+        v = float(self.loss.item())
+        self.check("last_loss")
+        return v
+
+    def params(self) -> torch.Tensor:
+        self.check("params", collective=True)
+        return self.p[:self.P].reshape(self.shape).clone()
+
+    def trajectory(self) -> torch.Tensor:
+        self.check("trajectory", collective=True)
+        if self.traj_loc is not None:
+            rows = self.step_host + 1
+            loc = self.traj_loc[:rows].contiguous()
+            gathered = torch.empty((self.size,) + tuple(loc.shape), dtype=loc.dtype,
+                                   device=self.device)
+            self.comm.all_gather_into_tensor(gathered.reshape(-1), loc.reshape(-1))
+            full = gathered.permute(1, 0, 2).reshape(rows, -1)[:, :self.P]
+            return full.reshape((rows,) + self.shape)
+        t = self.history.result()[:, :self.P] if self.history.mode == "full" else self.history.result()
+        return t.reshape((t.shape[0],) + self.shape)
+
+    def run_adam(self, guess, nsteps: int = 100, param_bounds=None, learning_rate: float = 0.01,
+                 b1: float = 0.9, b2: float = 0.999, eps: float = 1e-8, history="full",
+                 legacy_bounds_jacobian: bool = False, callback=None, **unused):
+        """Adam with the reference's contract: trajectory ``(nsteps+1, *shape)``."""
+        if unused:
+            raise TypeError(f"unsupported run_adam options for the graph engine: {sorted(unused)}")
+        from ..utils.hooks import StepHooks, driver_guard
+        self.setup(guess, nsteps, param_bounds, learning_rate, b1, b2, eps, history,
+                   legacy_bounds_jacobian)
+        hooks = StepHooks(self.comm, callback)
+        with driver_guard(self.comm):
+            for i in range(int(nsteps)):
+                self.step()
+                if hooks.active:
+                    hooks(i, self.loss, self, self.params)
+            return self.trajectory()

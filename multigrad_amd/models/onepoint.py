@@ -18,6 +18,7 @@ functions (see :mod:`multigrad_amd.models.smf`) or the fused-engine protocol
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 from typing import Any, Optional, Tuple, Union
 
@@ -84,13 +85,24 @@ class _OptimizerFrontEnds:
             def loss_and_grad_fn(x, _, **k):
                 return self.calc_loss_and_grad_from_params(x, **k)
         fused = getattr(self, "fused_engine", None)
-        if fused is not None and randkey is None and not const_randkey and \
-                kw.pop("use_engine", True):
+        use_engine = kw.pop("use_engine", True)
+        if fused is not None and randkey is None and not const_randkey and use_engine:
             eng = fused()
             if eng is not None:
                 return eng.run_adam(guess, nsteps=nsteps, param_bounds=param_bounds,
                                     learning_rate=learning_rate, **kw)
-        kw.pop("use_engine", None)
+        # any other model on a GPU: one captured step replayed per iteration
+        # (engine/generic.py), unless per-step keys or unsupported options need the loop
+        graph_kw = {k: kw[k] for k in kw if k in ("history", "legacy_bounds_jacobian", "b1",
+                                                   "b2", "eps", "callback")}
+        if fused is None and use_engine and randkey is None and not const_randkey and \
+                len(graph_kw) == len(kw) and guess.is_cuda and \
+                not getattr(self, "sumstats_func_has_aux", False) and \
+                os.environ.get("MULTIGRAD_GENERIC_ENGINE", "1") != "0":
+            from ..engine.generic import GraphAdamEngine
+            return GraphAdamEngine(self, comm=comm).run_adam(
+                guess, nsteps=nsteps, param_bounds=param_bounds, learning_rate=learning_rate,
+                **graph_kw)
         return _adam.run_adam(loss_and_grad_fn, params=guess, data=None, nsteps=nsteps,
                               param_bounds=param_bounds, learning_rate=learning_rate,
                               randkey=randkey, comm=comm, **kw)
