@@ -29,11 +29,18 @@ def main(argv=None):
     m = TorchPopulationSMFModel(aux_data=torch_population_data(data))
     guess = data["guess"]
     out = {}
+    tuned = {}
+
+    def _auto(n):
+        eng = GraphAdamEngine(m)
+        traj = eng.run_adam(guess, nsteps=n, learning_rate=1e-3)
+        tuned.update(eng.tuning or {"fallback": eng.fallback_reason})
+        return traj
     for name, fn in (("eager", lambda n: m.run_adam(guess, nsteps=n, learning_rate=1e-3,
                                                     use_engine=False)),
                      ("graph", lambda n: GraphAdamEngine(m, graph=True).run_adam(
                          guess, nsteps=n, learning_rate=1e-3)),
-                     ("auto", lambda n: m.run_adam(guess, nsteps=n, learning_rate=1e-3))):
+                     ("auto", lambda n: _auto(n))):
         fn(3)  # warm-up (kernel loading, capture)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -45,7 +52,8 @@ def main(argv=None):
                           "steps_per_s": round(a.steps / dt, 2), "halos": a.halos,
                           "final_param_0": float(traj[-1, 0])}), flush=True)
     print(json.dumps({"graph_speedup": round(out["graph"] / out["eager"], 3),
-                      "auto_speedup": round(out["auto"] / out["eager"], 3)}), flush=True)
+                      "auto_speedup": round(out["auto"] / out["eager"], 3),
+                      "auto_tuning": tuned}), flush=True)
 
 
 if __name__ == "__main__":

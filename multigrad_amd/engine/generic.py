@@ -139,7 +139,7 @@ class GraphAdamEngine:
             self.history = History(history, nsteps, self.p[:P].clone())
         self.graph = None
         self.tuning = None
-        self._times = {"eager": [], "graph": []}
+        self._times = {}
         capturable = cuda and (W == 1 or (self.twoshot is not None and self.oneshot is not None))
         if self.graph_req is True and not capturable:
             raise RuntimeError("this step is not capturable (RCCL collectives in it)")
@@ -229,13 +229,14 @@ class GraphAdamEngine:
 
     def _tuned_step(self):
         """Auto policy (``graph=None``): the first steps run eagerly, the next ones from
-        the captured graph, each timed; the faster mode is kept (a collective decision).
-        Graph replay wins when the step is launch bound (1.8x on a 1e4-parameter torch
-        model) and loses ~10% when it is GPU bound (1e6 parameters): both measured on
-        one MI355X (profiles/generic_engine.md)."""
+        the captured graph; each window of steps is timed as a whole (no synchronisation
+        inside it, so eager launches overlap the GPU as in steady state) and the faster
+        mode is kept -- a collective decision.  Measured on one MI355X
+        (profiles/generic_engine.md): replay wins when the step is launch bound (1.4-1.8x
+        on a 1e4-parameter torch model) and loses ~10% when it is GPU bound."""
         import time
-        k = self.step_host
-        mode = "eager" if k < self._TUNE else "graph"
+        k, T = self.step_host, self._TUNE
+        mode = "eager" if k < T else "graph"
         if mode == "graph" and self.graph is None:
             self.step_dev[0] = k   # eager steps keep the count on the host
             try:
@@ -248,16 +249,18 @@ class GraphAdamEngine:
                 self.fallback_reason = f"capture failed: {type(exc).__name__}: {exc}"
                 self._body(k)
                 return
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
+        if k in (0, T):
+            torch.cuda.synchronize()
+            self._t0 = time.perf_counter()
         if mode == "graph":
             self.graph.replay()
         else:
             self._body(k)
-        torch.cuda.synchronize()
-        self._times[mode].append(time.perf_counter() - t0)
-        if mode == "graph" and len(self._times["graph"]) == self._TUNE:
-            te, tg = min(self._times["eager"]), min(self._times["graph"])
+        if k in (T - 1, 2 * T - 1):
+            torch.cuda.synchronize()
+            self._times[mode] = time.perf_counter() - self._t0
+        if k == 2 * T - 1:
+            te, tg = self._times["eager"] / T, self._times["graph"] / T
             keep = 1 if tg < te else 0
             if self.size > 1:
                 keep = int(all(self.comm.allgather(keep)))
