@@ -65,6 +65,9 @@ def _args(argv=None):
                          "ranks, global otherwise)")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--profile-phases", action="store_true")
+    ap.add_argument("--no-count-launches", dest="count_launches", action="store_false",
+                    help="skip counting the device operations of one step (torch.profiler, "
+                         "after the timed region)")
     return ap.parse_args(argv)
 
 
@@ -113,8 +116,9 @@ def time_placement(placement, args, comm, dev, sync):
     if args.profile_phases:  # HIP-event timing per phase (eager launches)
         from multigrad_amd.utils.profiling import PhaseTimer
         engine.timer = PhaseTimer(True)
-    engine.setup(data["guess"], nsteps=args.warmup + args.steps, learning_rate=args.lr,
-                 history=history)
+    count = args.count_launches and dev.type == "cuda"
+    engine.setup(data["guess"], nsteps=args.warmup + args.steps + (2 if count else 0),
+                 learning_rate=args.lr, history=history)
     sync()
     setup_s = time.perf_counter() - t_setup
 
@@ -133,6 +137,12 @@ def time_placement(placement, args, comm, dev, sync):
     elapsed = time.perf_counter() - t0
     engine.check()  # a failed peer exchange raises here instead of reporting wrong numbers
     loss1 = engine.last_loss()
+    ops = {}
+    if count:  # after the timing: device operations of one steady-state step
+        from multigrad_amd.utils.profiling import count_device_ops
+        ops = count_device_ops(engine.step, 2)
+        engine.drain()
+        engine.check()
     if comm.size > 1:
         t = torch.tensor([elapsed], dtype=torch.float64)
         comm.all_reduce(t, op="max")
@@ -156,6 +166,7 @@ def time_placement(placement, args, comm, dev, sync):
         "loss_last": loss1,
         "setup_s": round(setup_s, 2),
         "history": history,
+        "device_ops_per_step": ops or None,
     }
     if args.profile_phases:
         info["phases_ms"] = {k: round(v, 4) for k, v in engine.timer.summary().items()}
@@ -232,6 +243,7 @@ def main(argv=None):
             "sumstat_allreduce": head["sumstat_allreduce"],
             "chunks": head["chunks"],
             "layout": head["layout"],
+            "device_ops_per_step": head["device_ops_per_step"],
         },
         "owner_steps_per_s": None if own is None else round(own["steps_per_s"], 3),
         "owner_ms_per_step": None if own is None else round(own["ms_per_step"], 4),
@@ -242,7 +254,8 @@ def main(argv=None):
     if own is not None and own is not head:
         rec["owner_config"] = {k: own[k] for k in ("parallelism", "optimizer_sharding",
                                                    "grad_collective", "sumstat_allreduce",
-                                                   "chunks", "pipelined", "layout")}
+                                                   "chunks", "pipelined", "layout",
+                                                   "device_ops_per_step")}
     if args.profile_phases:
         rec["phases_ms"] = head["phases_ms"]
         if own is not None and own is not head:

@@ -4,12 +4,14 @@ Reference: ``multigrad/mpi4jax/multigrad.py:17-61`` (``distribute_data``, in-gra
 ``reduce_sum`` via ``mpi4jax.allreduce``, and ``simple_grad_descent`` as a ``lax.scan``
 with in-graph collectives, returning a pandas DataFrame).
 
-Here the "graph" is a HIP graph: on a single GPU rank the whole step -- user loss/grad
-function, stream-ordered all-reduce, parameter update, and the writes of this step's
-loss and parameters into preallocated device histories -- is captured once with
-``torch.cuda.CUDAGraph`` and replayed ``nsteps`` times with no host work per step.  On
-several ranks (or on CPU) the same step runs eagerly; collectives are RCCL/gloo
-all-reduces enqueued on the compute stream.  Unlike the reference (update on rank 0 then
+Here the "graph" is a HIP graph: the whole step -- user loss/grad function, stream-ordered
+all-reduce, parameter update, and the writes of this step's loss and parameters into
+preallocated device histories -- is captured once with ``torch.cuda.CUDAGraph`` and
+replayed ``nsteps`` times with no host work per step.  On several GPU ranks the
+all-reduce is the two-shot peer-memory exchange (:meth:`~multigrad_amd.parallel.xgmi.
+TwoShot.all_reduce_`, device-side sequence numbers, so it replays inside the graph);
+where that is unavailable (fp64 values, ``MULTIGRAD_TWOSHOT=0``, CPU/gloo) the step runs
+eagerly with RCCL/gloo all-reduces enqueued on the compute stream.  Unlike the reference (update on rank 0 then
 bcast, which it notes is needed "probably due to a bug"), every rank applies the same
 all-reduced update.
 """
@@ -33,13 +35,27 @@ def distribute_data(data, comm=None):
     return _distribute_data(data, comm=get_world_comm() if comm is None else comm)
 
 
+def _device_allreduce(t: torch.Tensor, comm):
+    """The two-shot context that can sum ``t`` over ``comm`` inside a graph, or None."""
+    if comm.size < 2 or t.device.type != "cuda" or t.dtype != torch.float32:
+        return None
+    from .parallel.xgmi import get_twoshot_allreduce
+    return get_twoshot_allreduce(comm, t.numel())
+
+
 def reduce_sum(partial_value: torch.Tensor, comm=None) -> torch.Tensor:
-    """Stream-ordered in-place-safe sum over ranks (capturable into a HIP graph)."""
+    """Stream-ordered sum over ranks, returning a new tensor.  fp32 CUDA values on several
+    ranks go through the two-shot peer-memory exchange, which is capturable into a HIP
+    graph and bitwise identical on every rank; others use ``comm.all_reduce``."""
     comm = get_world_comm() if comm is None else comm
     out = partial_value.clone() if not partial_value.is_contiguous() else partial_value
     if comm.size > 1:
         out = out.clone()
-        comm.all_reduce(out)
+        ts = _device_allreduce(out, comm)
+        if ts is not None:
+            ts.all_reduce_(out)
+        else:
+            comm.all_reduce(out)
     return out
 
 
@@ -61,7 +77,11 @@ def simple_grad_descent(data_dict, loss_and_grad_func: Callable, guess, learning
     losses = torch.zeros(n, dtype=params.dtype, device=dev)
     hist = torch.zeros((n,) + tuple(params.shape), dtype=params.dtype, device=dev)
     step = torch.zeros((), dtype=torch.long, device=dev)
-    use_graph = (dev.type == "cuda" and comm.size == 1) if graph is None else bool(graph)
+    # several ranks: capturable only when the loss/grad vector can take the two-shot path
+    ts = _device_allreduce(torch.empty(1 + params.numel(), dtype=params.dtype, device=dev), comm)
+    if graph is None:
+        graph = dev.type == "cuda" and (comm.size == 1 or ts is not None)
+    use_graph = bool(graph)
 
     def body():
         loss, grad = loss_and_grad_func(data_dict, params)
@@ -88,14 +108,19 @@ def simple_grad_descent(data_dict, loss_and_grad_func: Callable, guess, learning
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
                 body()
-            for _ in range(n):
-                g.replay()
             done = True
         except RuntimeError:
             # the user function is not capturable (host sync, dynamic shapes): run eagerly
             torch.cuda.synchronize()
             params.copy_(saved)
             step.zero_()
+        if comm.size > 1 and not all(comm.allgather(done)):
+            done = False  # every rank replays or none does (same collective sequence)
+            params.copy_(saved)
+            step.zero_()
+        if done:
+            for _ in range(n):
+                g.replay()
     if not done:
         hooks = StepHooks(comm)  # MULTIGRAD_CHECK_EVERY / MULTIGRAD_METRICS (eager steps)
         with driver_guard(comm):
@@ -103,6 +128,8 @@ def simple_grad_descent(data_dict, loss_and_grad_func: Callable, guess, learning
                 body()
                 if hooks.active:
                     hooks(i, losses[i], None, lambda: params)
+    if ts is not None:
+        ts.check("ingraph.simple_grad_descent", comm)  # a timed-out exchange raises here
     loss_np = losses.detach().cpu().numpy()
     par_np = hist.detach().cpu().numpy()
     return pd.DataFrame(dict(loss=list(loss_np), params=list(par_np)))

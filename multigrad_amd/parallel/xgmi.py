@@ -285,6 +285,26 @@ class TwoShot:
     def check(self, where: str = "", comm=None) -> None:
         OneShotAllReduce.check(self, where, comm)  # same err/seq protocol words
 
+    def all_reduce_(self, t: torch.Tensor) -> torch.Tensor:
+        """In-place sum of a contiguous fp32 tensor of at most ``numel`` elements over the
+        ranks, stream ordered and graph capturable (mode-0 exchange: every rank sums the
+        peers' slices in rank order, so all ranks get bitwise identical results).
+
+        Reusing the regions across calls is safe without host syncs: an exchange returns
+        only when every peer has pulled this rank's ``grad`` and pushed into its ``theta``,
+        and a peer's next exchange waits for this rank's next launch, which follows this
+        rank's copy-out in stream order."""
+        k = t.numel()
+        if k > self.numel or t.dtype != torch.float32 or not t.is_contiguous():
+            raise ValueError("two-shot all_reduce_: contiguous fp32 tensor of at most "
+                             f"{self.numel} elements expected, got {t.dtype} x {k}")
+        flat = t.view(-1)
+        self.grad[:k].copy_(flat)
+        lo, n = self.slice()
+        self.step(lo, n, 0)
+        flat.copy_(self.theta[:k])
+        return t
+
     def ok(self) -> bool:
         return int(self.err.item()) == 0
 
@@ -332,6 +352,27 @@ class TwoShot:
             E.xgmi_free(b)
         self.regions = ()
         self.grad = self.theta = None
+
+
+def get_twoshot_allreduce(comm, numel: int) -> Optional[TwoShot]:
+    """A cached two-shot context able to sum ``numel`` fp32 values over ``comm`` (for
+    capturable user-level all-reduces, :func:`multigrad_amd.ingraph.reduce_sum`);
+    collective on first use for a given size class.  None when disabled or unavailable
+    (the caller uses RCCL)."""
+    if (comm is None or comm.size < 2 or comm.size > MAX_RANKS or not twoshot_enabled()
+            or not torch.cuda.is_available()):
+        return None
+    quantum = 4 * comm.size
+    want = max(quantum, -(-int(numel) // quantum) * quantum)
+    cache = getattr(comm, "_twoshot_ar", None)
+    if cache is None:
+        cache = comm._twoshot_ar = {}
+    for have, ts in cache.items():
+        if have >= want:
+            return ts or None
+    ts = connect_twoshot(comm, want, _timeout_s()) or False
+    cache[want] = ts
+    return ts or None
 
 
 def connect_twoshot(comm, numel: int, timeout_s: Optional[float] = None,

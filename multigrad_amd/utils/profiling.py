@@ -65,3 +65,29 @@ def torch_profile(path: str = "gpurun_out/torch_trace.json", **kw):
         yield prof
     os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
     prof.export_chrome_trace(path)
+
+
+def count_device_ops(fn, reps: int = 2) -> dict:
+    """Device operations per call of ``fn`` (kernels, copies, fills), counted with
+    ``torch.profiler`` over ``reps`` calls -- graph replays included, since the tracer sees
+    each dispatched kernel.  Returns ``{"kernels": k, "memcpy": c, "memset": s}`` per call,
+    or ``{}`` when the profiler cannot trace the device."""
+    if not torch.cuda.is_available():
+        return {}
+    torch.cuda.synchronize()
+    try:
+        with torch.profiler.profile(activities=[torch.profiler.ProfilerActivity.CUDA]) as prof:
+            for _ in range(reps):
+                fn()
+            torch.cuda.synchronize()
+        counts = collections.Counter()
+        for e in prof.events():
+            if e.device_type != torch.autograd.DeviceType.CUDA:
+                continue
+            name = e.name.lower()
+            kind = ("memcpy" if "memcpy" in name or "copy" in name and "kernel" not in name
+                    else "memset" if "memset" in name or "fill_buffer" in name else "kernels")
+            counts[kind] += 1
+    except Exception:  # noqa: BLE001 -- a tracer problem must not fail the caller
+        return {}
+    return {k: round(counts[k] / reps, 2) for k in ("kernels", "memcpy", "memset")}

@@ -218,3 +218,44 @@ def test_twoshot_late_peer_fails_loudly():
     np.testing.assert_array_equal(a0, np.full(1024, 3.0, dtype=np.float32))
     np.testing.assert_array_equal(a1, a0)
     assert ok0 and ok1
+
+
+def _ingraph(rank, size, graph):
+    import multigrad_amd as mg
+    from multigrad_amd import ingraph
+    comm = mg.get_world_comm()
+    if graph is False:  # the RCCL path for comparison
+        os.environ["MULTIGRAD_TWOSHOT"] = "0"
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn(4000, generator=g).cuda()
+    data = dict(x=ingraph.distribute_data(x, comm))
+
+    def loss_and_grad(d, p):  # sum over ranks of 0.5 * |x - p|^2 / N per coordinate
+        r = d["x"][:, None] - p[None, :]
+        return 0.5 * (r * r).sum() / x.numel(), -r.sum(0) / x.numel()
+
+    guess = torch.tensor([0.5, -1.0, 2.0], device="cuda")
+    df = ingraph.simple_grad_descent(data, loss_and_grad, guess, learning_rate=0.3,
+                                     nsteps=20, comm=comm, graph=None)
+    cached = getattr(comm, "_twoshot_ar", {})
+    return (np.stack(df["params"].to_numpy()), np.asarray(df["loss"], dtype=np.float64),
+            any(bool(v) for v in cached.values()))
+
+
+def test_ingraph_descent_multirank_captured_matches_rccl():
+    """ingraph.simple_grad_descent on two ranks: graph-captured with the two-shot all-reduce
+    by default, matching the eager RCCL path and the closed-form descent."""
+    out = run_distributed(_ingraph, 2, None, timeout=300)
+    ref = run_distributed(_ingraph, 2, False, timeout=300)
+    for (p, l, used), (pr, lr_, used_r) in zip(out, ref):
+        assert used and not used_r
+        np.testing.assert_allclose(p, pr, rtol=1e-5, atol=1e-6)
+        np.testing.assert_allclose(l, lr_, rtol=1e-5, atol=1e-7)
+    np.testing.assert_array_equal(out[0][0], out[1][0])  # same bits on both ranks
+    # closed form: p_{k+1} = p_k - 0.3 (p_k - mean x)
+    g = torch.Generator().manual_seed(11)
+    mean = float(torch.randn(4000, generator=g).double().mean())
+    p = np.array([0.5, -1.0, 2.0])
+    for k in range(20):
+        np.testing.assert_allclose(out[0][0][k], p, rtol=1e-4, atol=1e-5)
+        p = p - 0.3 * (p - mean)
