@@ -23,6 +23,7 @@
 // 2-parameter shared-parameter models).
 #include "common.h"
 #include "xgmi.h"
+#include "tail_table.h"
 
 #include <torch/extension.h>
 #include <ATen/hip/HIPContext.h>
@@ -61,6 +62,51 @@ __device__ __forceinline__ float inv_sigma(float s) {
   return LOGSIG ? fast_exp2(-s * kLog2_10) : 1.0f / s;
 }
 
+// Table path of the absolute contract (MG_FWD_TAB): the signed tail V(n) = sign(n) Q(|n|)
+// is read from a piecewise-cubic table (tail_table.h, tools/fit_tail_table.py: 96 pieces
+// over |z| <= 6, float32 chain error 8.8e-8 against 1.6e-7 for the rational polynomial)
+// held in LDS, instead of v_rcp + a degree-5 Horner chain + the product with exp2(-w^2):
+//   t = clamp(n * INVH), k = floor(t) (v_cvt_flr), s = fract(t), V = c_k(s)
+// The exponential is still evaluated for the residuals G, W (unchanged semantics) but no
+// longer for the forward sums.  The integer part is counted from t < 0, so it always
+// agrees with the piece that was read (the jump of V at n = 0 is a piece boundary).
+// LDS layout: REPL replicas of every entry, lane l reading replica l % REPL, so the 16
+// lanes of a ds_read_b128 lane group hit distinct bank quads (REPL = 16: conflict free;
+// 8: two lanes per replica).
+// MG_FWD_TAB = 1 (default): forwards WITHOUT residuals use the table -- there it also
+// removes the v_exp, and the lanes forward measured 440 vs 536-540 us at 1.34e8 halos.
+// MG_FWD_TAB = 2 also uses it in the residual forwards, where the exponential stays (for
+// G, W): measured slower there (pipelined 702 vs 628 us, residual 620 vs 570 us).  The
+// index arithmetic (v_med3, v_cvt_flr, v_fract, v_lshl_or: 4.2-4.3 cycles per wave each,
+// tools/ubench/op_rates.hip, against 2.7 for v_fma) eats most of what the v_rcp and the
+// Horner chain cost, and at 119-128 VGPRs the compiler waits for each table read right
+// after issuing it (docs/design.md, forward floor).
+#ifndef MG_FWD_TAB
+#define MG_FWD_TAB 1
+#endif
+__device__ __forceinline__ int cvt_flr_i32(float t) {
+  int k;
+  asm("v_cvt_flr_i32_f32 %0, %1" : "=v"(k) : "v"(t));
+  return k;
+}
+
+__device__ __forceinline__ float fma_scalar(float a, float b, float c) {
+  float d;
+  asm("v_fma_f32 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+  return d;
+}
+
+template <int REPL>
+__device__ __forceinline__ void tail_tab_fill(float4* tab) {
+  for (int i = threadIdx.x; i < kTailTabN * REPL; i += blockDim.x) tab[i] = g_tail_tab[i / REPL];
+}
+
+// this lane's view of the LDS table: entry k in [-N/2, N/2) at tb[k * REPL]
+template <int REPL>
+__device__ __forceinline__ const float4* tail_tab_lane(const float4* tab) {
+  return tab + (kTailTabN / 2) * REPL + (threadIdx.x & (REPL - 1));
+}
+
 // Accumulate the NB bin masses of one halo.
 // Work with the negated scaled coordinate n_e = -w_e = (mu - e_e) * kWScale / sigma.
 // With signed tails V_e = copysign(Q(|z_e|), n_e) and pos_e = [n_e < 0] = [z_e > 0]
@@ -70,14 +116,24 @@ __device__ __forceinline__ float inv_sigma(float s) {
 // counts; the per-bin differences are formed once per thread at the end.
 // A halo with x = -inf contributes exactly zero (used to mask the unrolled tail): every
 // V_e is -0 and every pos_e is 1, which cancels in the differences.
-template <int NB, bool LOGSIG, bool REL>
+template <int NB, bool LOGSIG, bool REL, int REPL = 0>
 __device__ __forceinline__ void halo_mass(float x, float2 th, const SmfBins& b,
-                                          float (&acc)[NB + 1], int (&cnt)[NB + 1]) {
+                                          float (&acc)[NB + 1], int (&cnt)[NB + 1],
+                                          const float4* __restrict__ tb = nullptr) {
   const float ninv = -inv_sigma<LOGSIG>(th.y) * kWScale;
   const float mu = -(x + th.x) * ninv;  // = (x + a) * kWScale / sigma
 #pragma unroll
   for (int e = 0; e <= NB; ++e) {
     const float n = fmaf(b.edge[e], ninv, mu);
+    if constexpr (REPL > 0) {  // signed-tail table (see ep_eval_tab)
+      const float t = __builtin_amdgcn_fmed3f(n * kTailTabInvH, -(float)(kTailTabN / 2),
+                                              (float)(kTailTabN / 2) - 1.0f / 4096);
+      const float4 c = tb[cvt_flr_i32(t) * REPL];
+      const float s = __builtin_amdgcn_fractf(t);
+      acc[e] += fma_scalar(fma_scalar(fma_scalar(c.w, s, c.z), s, c.y), s, c.x);
+      cnt[e] += __builtin_popcountll(__builtin_amdgcn_ballot_w64(t < 0.0f));
+      continue;
+    }
     float p, g;
     normal_tail_parts_w<REL>(n, p, g);
     acc[e] = fmaf(p, __builtin_copysignf(g, n), acc[e]);
@@ -104,6 +160,15 @@ __global__ __launch_bounds__(kThreads, MG_FWD_MINWAVES) void smf_fwd_kernel(
     const float* __restrict__ x, const int32_t* __restrict__ pop,
     const float2* __restrict__ theta, int64_t begin, int64_t end, SmfBins bins,
     float* __restrict__ slab) {
+  // signed-tail table: 8 replicas (8 workgroups per CU share the LDS)
+  constexpr int kRepl = (!REL && MG_FWD_TAB >= 1 && MG_FWD_BALLOT) ? 8 : 0;
+  const float4* tb = nullptr;
+  if constexpr (kRepl > 0) {
+    __shared__ float4 tab[kTailTabN * (kRepl > 0 ? kRepl : 1)];
+    tail_tab_fill<kRepl>(tab);
+    __syncthreads();
+    tb = tail_tab_lane<kRepl>(tab);
+  }
   float acc[NB + 1];
   int cnt[NB + 1];
 #pragma unroll
@@ -132,7 +197,8 @@ __global__ __launch_bounds__(kThreads, MG_FWD_MINWAVES) void smf_fwd_kernel(
 #pragma unroll
     for (int u = 0; u < kFwdUnroll; ++u) ths[u] = HAS_POP ? theta[ps[u]] : th0;
 #pragma unroll
-    for (int u = 0; u < kFwdUnroll; ++u) halo_mass<NB, LOGSIG, REL>(xs[u], ths[u], bins, acc, cnt);
+    for (int u = 0; u < kFwdUnroll; ++u)
+      halo_mass<NB, LOGSIG, REL, kRepl>(xs[u], ths[u], bins, acc, cnt, tb);
   }
 #if MG_FWD_BALLOT
   const bool counter = lane == 0;  // the counts are per wave: fold them in once
@@ -562,13 +628,52 @@ __device__ __forceinline__ void ep_eval(v2f n, v2f (&acc)[EdgePairs<NB>::NV],
   }
 }
 
-template <int NB, bool LOGSIG, bool REL, bool RESID>
+template <int NB, bool RESID, int REPL>
+__device__ __forceinline__ void ep_eval_tab(v2f n, const float4* __restrict__ tb,
+                                            v2f (&acc)[EdgePairs<NB>::NV],
+                                            v2f (&G)[EdgePairs<NB>::NV], v2f (&W)[EdgePairs<NB>::NV],
+                                            int i, int& ca, int& cb) {
+  constexpr float kLo = -(float)(kTailTabN / 2);
+  constexpr float kHi = (float)(kTailTabN / 2) - 1.0f / 4096;
+  v2f t = n * kTailTabInvH;
+  t.x = __builtin_amdgcn_fmed3f(t.x, kLo, kHi);
+  t.y = __builtin_amdgcn_fmed3f(t.y, kLo, kHi);
+  const float4 cx = tb[cvt_flr_i32(t.x) * REPL];
+  const float4 cy = tb[cvt_flr_i32(t.y) * REPL];
+  const float sx = __builtin_amdgcn_fractf(t.x);
+  const float sy = __builtin_amdgcn_fractf(t.y);
+  // scalar Horner on purpose: packing the two chains would need a v_mov per operand pair
+  // (the coefficients of the two elements come from different table reads)
+  v2f v;
+  v.x = fma_scalar(fma_scalar(fma_scalar(cx.w, sx, cx.z), sx, cx.y), sx, cx.x);
+  v.y = fma_scalar(fma_scalar(fma_scalar(cy.w, sy, cy.z), sy, cy.y), sy, cy.x);
+  acc[i] = acc[i] + v;
+  ca += __builtin_popcountll(__builtin_amdgcn_ballot_w64(t.x < 0.0f));
+  cb += __builtin_popcountll(__builtin_amdgcn_ballot_w64(t.y < 0.0f));
+  if constexpr (RESID) {
+    const v2f e = -n * n;
+    v2f g;
+    g.x = fast_exp2(e.x);
+    g.y = fast_exp2(e.y);
+    G[i] = G[i] + g;
+    W[i] = (-g) * n + W[i];
+  }
+}
+
+template <int NB, bool LOGSIG, bool REL, bool RESID, int REPL = 0>
 __device__ __forceinline__ void lane_halo_ep(float x0, float x1, float ninv, float mua,
                                              const SmfBins& b,
                                              v2f (&acc)[EdgePairs<NB>::NV], int (&cnt)[NB + 1],
                                              v2f (&G)[EdgePairs<NB>::NV],
-                                             v2f (&W)[EdgePairs<NB>::NV]) {
+                                             v2f (&W)[EdgePairs<NB>::NV],
+                                             const float4* tb = nullptr) {
   using E = EdgePairs<NB>;
+  auto eval = [&](v2f n, int i, int& ca, int& cb) {
+    if constexpr (REPL > 0)
+      ep_eval_tab<NB, RESID, REPL>(n, tb, acc, G, W, i, ca, cb);
+    else
+      ep_eval<NB, REL, RESID>(n, acc, G, W, i, ca, cb);
+  };
   const float mu0 = fmaf(x0, -ninv, mua);
   const float mu1 = fmaf(x1, -ninv, mua);
 #pragma unroll
@@ -580,7 +685,7 @@ __device__ __forceinline__ void lane_halo_ep(float x0, float x1, float ninv, flo
       e2.x = b.edge[2 * i];
       e2.y = b.edge[2 * i + 1];
       const v2f n = e2 * ninv + mu;
-      ep_eval<NB, REL, RESID>(n, acc, G, W, i, cnt[2 * i], cnt[2 * i + 1]);
+      eval(n, i, cnt[2 * i], cnt[2 * i + 1]);
     }
   }
   if constexpr (E::NX) {
@@ -589,7 +694,7 @@ __device__ __forceinline__ void lane_halo_ep(float x0, float x1, float ninv, flo
     m2.y = mu1;
     const v2f n = (v2f)(b.edge[E::NE - 1] * ninv) + m2;
     int c2 = 0;
-    ep_eval<NB, REL, RESID>(n, acc, G, W, E::NP, cnt[E::NE - 1], c2);
+    eval(n, E::NP, cnt[E::NE - 1], c2);
     cnt[E::NE - 1] += c2;
   }
 }
@@ -739,6 +844,17 @@ __global__ __launch_bounds__(kThreads, MG_LANES_MINWAVES) void smf_fwd_lanes_ker
     const int32_t* __restrict__ wave_start, int* __restrict__ queues, int nq,
     LanesUpdate upd = LanesUpdate{}) {
   static_assert(!UPD || RESID, "the pipelined update reads the residuals it overwrites");
+  // signed-tail table (absolute contract): 16 replicas (conflict-free reads), 8 next to
+  // the pipelined update's staging buffer (LDS budget of 4 workgroups per CU)
+  constexpr int kRepl =
+      (!REL && MG_LANES_EP && (MG_FWD_TAB >= 2 || (MG_FWD_TAB == 1 && !RESID))) ? (UPD ? 8 : 16) : 0;
+  const float4* tb = nullptr;
+  if constexpr (kRepl > 0) {
+    __shared__ float4 tab[kTailTabN * (kRepl > 0 ? kRepl : 1)];
+    tail_tab_fill<kRepl>(tab);
+    __syncthreads();
+    tb = tail_tab_lane<kRepl>(tab);
+  }
   float acc[NB + 1];
   int cnt[NB + 1];
 #pragma unroll
@@ -967,7 +1083,8 @@ __global__ __launch_bounds__(kThreads, MG_LANES_MINWAVES) void smf_fwd_lanes_ker
 #if MG_LANES_EP
 #pragma unroll
       for (int u = 0; u < kLanesUnroll; u += 2)
-        lane_halo_ep<NB, LOGSIG, REL, RESID>(xc[u], xc[u + 1], ninv, mua, bins, accp, cnt, Gp, Wp);
+        lane_halo_ep<NB, LOGSIG, REL, RESID, kRepl>(xc[u], xc[u + 1], ninv, mua, bins, accp, cnt,
+                                                    Gp, Wp, tb);
 #elif MG_LANES_V2
       static_assert(kLanesUnroll % 2 == 0, "packed path takes halo pairs");
 #pragma unroll

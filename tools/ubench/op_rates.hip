@@ -6,6 +6,8 @@
 //   add_abs  v_add_f32 |x|+c           bfi      v_bfi_b32 (copysign)
 //   cmp_cnt  v_cmp + s_bcnt1 + s_add (ballot count; VALU->SALU dependency)
 //   exp_fma  1 exp : 4 fma mix         cndadd   v_cndmask-free count: cnt += x<0
+//   fract    v_fract_f32               cvt_flr  v_cvt_flr_i32_f32
+//   med3     v_med3_f32                lshl_or  v_lshl_or_b32
 #include <hip/hip_runtime.h>
 #include <cstdio>
 
@@ -38,6 +40,18 @@ __global__ __launch_bounds__(256) void k(float* out, float seed) {
         else a[j] = __builtin_fmaf(a[j], 0.999f, 1e-7f);
       }
       if constexpr (KIND == 8) ci[j] += (a[j] < (float)it) ? 1 : 0;
+      if constexpr (KIND == 9) a[j] = __builtin_amdgcn_fractf(a[j]);
+      if constexpr (KIND == 10) {
+        int kk;
+        asm volatile("v_cvt_flr_i32_f32 %0, %1" : "=v"(kk) : "v"(a[j]));
+        a[j] = __int_as_float(kk);
+      }
+      if constexpr (KIND == 11) a[j] = __builtin_amdgcn_fmed3f(a[j], -3.0f, seed);
+      if constexpr (KIND == 12) {
+        int kk;
+        asm volatile("v_lshl_or_b32 %0, %1, 8, %2" : "=v"(kk) : "v"(ci[j]), "v"(cnt));
+        ci[j] = kk;
+      }
     }
   }
   float s = (float)cnt;
@@ -68,14 +82,17 @@ int main() {
   hipDeviceProp_t p;
   (void)hipGetDeviceProperties(&p, 0);
   const int blocks = p.multiProcessorCount * 8;  // 8 blocks x 4 waves = 32 waves/CU
-  const char* names[] = {"fma", "pk_fma", "exp", "rcp", "add_abs", "bfi", "cmp_cnt", "exp1fma3", "cndadd"};
-  float ms[9] = {run<0>(blocks, d), run<1>(blocks, d), run<2>(blocks, d), run<3>(blocks, d),
-                 run<4>(blocks, d), run<5>(blocks, d), run<6>(blocks, d), run<7>(blocks, d),
-                 run<8>(blocks, d)};
+  const char* names[] = {"fma", "pk_fma", "exp", "rcp", "add_abs", "bfi", "cmp_cnt", "exp1fma3",
+                         "cndadd", "fract", "cvt_flr", "med3", "lshl_or"};
+  constexpr int NK = 13;
+  float ms[NK] = {run<0>(blocks, d), run<1>(blocks, d), run<2>(blocks, d), run<3>(blocks, d),
+                  run<4>(blocks, d), run<5>(blocks, d), run<6>(blocks, d), run<7>(blocks, d),
+                  run<8>(blocks, d), run<9>(blocks, d), run<10>(blocks, d), run<11>(blocks, d),
+                  run<12>(blocks, d)};
   const double wave_instr = (double)blocks * 4 * kIters * 8;
   const double per_simd = wave_instr / (p.multiProcessorCount * 4);
   printf("clock %d kHz, %d CUs\n", p.clockRate, p.multiProcessorCount);
-  for (int i = 0; i < 9; ++i)
+  for (int i = 0; i < NK; ++i)
     printf("%-9s %.3f ms  %.3f ns per loop-body op per SIMD (%.2f cycles @2.4GHz)\n", names[i], ms[i],
            ms[i] * 1e6 / per_simd, ms[i] * 1e6 / per_simd * 2.4);
   return 0;
