@@ -26,6 +26,7 @@ L-BFGS-B projection semantics remain available through :func:`multigrad_amd.opti
 from __future__ import annotations
 
 import math
+import os
 from typing import Callable, Optional
 
 import numpy as np
@@ -104,10 +105,17 @@ def lbfgs_minimize(obj, maxiter: int = 100, m: int = 10, ftol: float = 1e7 * _EP
     dev = obj.device
     x = obj.x0().contiguous()
     f, g = obj(x)
-    g = g.clone()
+    g = g.clone()  # the objective may return a view of a buffer the next evaluation reuses
     nfev = 1
-    HS = torch.zeros((2 * m, n), dtype=torch.float32, device=dev)  # rows: S slots, Y slots
-    dot = MultiDot(2 * m, n, dev)
+    # rows 0..2m-1: the S and Y slots; 2m, 2m+1: the new pair s, y; 2m+2: the new gradient.
+    # One multi-dot of all rows against (s, y, g) gives every scalar an iteration needs
+    # (s.y, y.y, the new Gram rows, S^T g, Y^T g, g.g), and max|g| rides along in the same
+    # device->host copy: with the line search's one copy per evaluation, a typical
+    # iteration makes two.
+    HX = torch.zeros((2 * m + 3, n), dtype=torch.float32, device=dev)
+    HS = HX[:2 * m]
+    s_vec, y_vec, g_row = HX[2 * m], HX[2 * m + 1], HX[2 * m + 2]
+    dot = MultiDot(2 * m + 3, n, dev)
     dot1 = MultiDot(1, n, dev)
     SY = np.zeros((m, m))
     YY = np.zeros((m, m))
@@ -116,28 +124,34 @@ def lbfgs_minimize(obj, maxiter: int = 100, m: int = 10, ftol: float = 1e7 * _EP
     order: list = []  # ring slots, oldest -> newest
     d = torch.empty_like(x)
     xt = torch.empty_like(x)
-    sy_buf = torch.empty((2, n), dtype=torch.float32, device=dev)  # rows: s_new, y_new
     dev_call = getattr(obj, "device_call", None) if dev.type == "cuda" else None
-    dot_sy = MultiDot(2, n, dev)
     coef = torch.zeros(2 * m, dtype=torch.float32, device=dev)
+    gmax_dev = torch.zeros(1, dtype=torch.float64, device=dev)
 
     def gdot(a: torch.Tensor, b: torch.Tensor) -> float:
         v = dot1(a.view(1, -1), 1, [b]).cpu().numpy().reshape(-1)
         return float(_allreduce_np(comm, v, sharded=sharded)[0])
 
-    def ginf(v: torch.Tensor) -> float:
-        loc = np.array([float(v.abs().max()) if v.numel() else 0.0])
-        return float(_allreduce_np(comm, loc, op="max", sharded=sharded)[0])
+    def gstats(gv: torch.Tensor):
+        """(global g.g, global max|g|) in one copy."""
+        gg_loc = dot1(gv.view(1, -1), 1, [gv]).reshape(1)
+        gmax_dev.copy_(gv.abs().max().reshape(1) if gv.numel() else gmax_dev.zero_())
+        h = torch.cat([gg_loc, gmax_dev]).cpu().numpy()
+        return (float(_allreduce_np(comm, h[:1], sharded=sharded)[0]),
+                float(_allreduce_np(comm, h[1:], op="max", sharded=sharded)[0]))
 
     status, message = 1, "STOP: TOTAL NO. of ITERATIONS REACHED LIMIT"
     nit = 0
     from ..utils.hooks import StepHooks
     hooks = StepHooks(comm, what="L-BFGS iterate")  # MULTIGRAD_CHECK_EVERY / _METRICS
-    if ginf(g) <= gtol:
+    gg, gmax = gstats(g)
+    if gmax <= gtol:
         status, message = 0, "CONVERGENCE: NORM_OF_PROJECTED_GRADIENT_<=_PGTOL"
     else:
         for k in range(maxiter):
-            # ---------------- search direction (compact inverse-Hessian product)
+            # ---------------- search direction (compact inverse-Hessian product); g.d
+            # follows from the host copies of S^T g, Y^T g and g.g (no device round trip)
+            gd = -gg
             if order:
                 idx = np.array(order)
                 gamma, a, b = compact_coefficients(SY, YY, Sg, Yg, order)
@@ -146,13 +160,13 @@ def lbfgs_minimize(obj, maxiter: int = 100, m: int = 10, ftol: float = 1e7 * _EP
                 cvec[m + idx] = -gamma * b
                 coef.copy_(torch.from_numpy(cvec.astype(np.float32)))
                 lincomb_(HS, 2 * m, coef, -gamma, g, d)
+                gd = -gamma * gg - float(a @ Sg[idx]) - gamma * float(b @ Yg[idx])
             else:
                 d.copy_(-g)
-            gd = gdot(g, d)
             if not np.isfinite(gd) or gd >= 0:  # not a descent direction: reset memory
                 order.clear()
                 d.copy_(-g)
-                gd = gdot(g, d)
+                gd = -gg
             a1 = 1.0 if order else min(1.0, 1.0 / math.sqrt(max(-gd, 1e-300)))
             # ---------------- strong-Wolfe line search
             cache = {}
@@ -201,41 +215,43 @@ def lbfgs_minimize(obj, maxiter: int = 100, m: int = 10, ftol: float = 1e7 * _EP
                 best = min(cands)[1]
             f_new, g_new, _ = cache[best]
             # ---------------- update iterate and history
-            s_vec, y_vec = sy_buf[0], sy_buf[1]
             torch.mul(d, best, out=s_vec)
             x.add_(s_vec)
             torch.sub(g_new, g, out=y_vec)
+            g_row.copy_(g_new)
             nit = k + 1
-            # s.y and y.y in one pass and one reduction
-            syy = _allreduce_np(comm, dot_sy(sy_buf, 2, [y_vec]).cpu().numpy().reshape(-1),
-                                sharded=sharded)
-            sy_new, yy_new = float(syy[0]), float(syy[1])
+            dv = dot(HX, 2 * m + 3, [s_vec, y_vec, g_row])  # (2m+3, 3)
+            gmax_dev.copy_(g_new.abs().max().reshape(1) if g_new.numel() else gmax_dev.zero_())
+            host = torch.cat([dv.reshape(-1), gmax_dev]).cpu().numpy()
+            dots = _allreduce_np(comm, host[:-1], sharded=sharded).reshape(2 * m + 3, 3)
+            gmax = float(_allreduce_np(comm, host[-1:], op="max", sharded=sharded)[0])
+            sy_new, yy_new = float(dots[2 * m, 1]), float(dots[2 * m + 1, 1])
+            gg = float(dots[2 * m + 2, 2])
             inserted = sy_new > _EPS * yy_new and yy_new > 0
             if inserted:
                 q = order.pop(0) if len(order) == m else min(set(range(m)) - set(order))
                 HS[q].copy_(s_vec)
                 HS[m + q].copy_(y_vec)
                 order.append(q)
-                dots = dot(HS, 2 * m, [HS[q], HS[m + q], g_new]).cpu().numpy()
-            else:
-                dots = dot(HS, 2 * m, [g_new]).cpu().numpy()
-            dots = _allreduce_np(comm, dots, sharded=sharded)
-            if inserted:
                 for o in order:
-                    SY[o, q] = dots[o, 1]          # s_o . y_q
-                    SY[q, o] = dots[m + o, 0]      # s_q . y_o
-                    YY[o, q] = YY[q, o] = dots[m + o, 1]
-                Sg[:] = dots[:m, 2]
-                Yg[:] = dots[m:, 2]
-            else:
-                Sg[:] = dots[:m, 0]
-                Yg[:] = dots[m:, 0]
+                    if o == q:
+                        SY[q, q] = sy_new
+                        YY[q, q] = yy_new
+                    else:
+                        SY[o, q] = dots[o, 1]          # s_o . y_new
+                        SY[q, o] = dots[m + o, 0]      # s_new . y_o
+                        YY[o, q] = YY[q, o] = dots[m + o, 1]
+            Sg[:] = dots[:m, 2]
+            Yg[:] = dots[m:2 * m, 2]
+            if inserted:
+                Sg[q] = dots[2 * m, 2]
+                Yg[q] = dots[2 * m + 1, 2]
             f_old, f, g = f, f_new, g_new
             if callback is not None:
                 callback(obj.full(x))
             if hooks.active:
                 hooks(k, f, None, (lambda: x) if not sharded else None)
-            if ginf(g) <= gtol:
+            if gmax <= gtol:
                 status, message = 0, "CONVERGENCE: NORM_OF_PROJECTED_GRADIENT_<=_PGTOL"
                 break
             if (f_old - f) <= ftol * max(abs(f_old), abs(f), 1.0):

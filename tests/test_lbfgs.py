@@ -37,6 +37,27 @@ def test_lbfgs_rosenbrock_matches_scipy_minimum():
     assert res.fun < 1e-6 and abs(res.nit - ref.nit) < 60
 
 
+def test_lbfgs_objective_returning_a_reused_buffer():
+    """An objective that returns a view of one gradient buffer (as the engine objective
+    does) must give the same iterates as one that returns fresh tensors."""
+    buf = torch.zeros(4)
+
+    class Fresh(L.GenericObjective):
+        pass
+
+    class Reused(L.GenericObjective):
+        def __call__(self, u):
+            f, g = super().__call__(u)
+            buf.copy_(g)
+            return f, buf
+
+    x0 = torch.tensor([-1.2, 1.0, -0.5, 0.8])
+    a = L.lbfgs_minimize(Fresh(_rosen_lg, x0), maxiter=30)
+    b = L.lbfgs_minimize(Reused(_rosen_lg, x0), maxiter=30)
+    assert a.nit == b.nit and a.nfev == b.nfev
+    np.testing.assert_array_equal(a.x.numpy(), b.x.numpy())
+
+
 def test_compact_direction_equals_two_loop():
     """The compact inverse-Hessian product equals the classical two-loop recursion."""
     rng = np.random.default_rng(0)
