@@ -165,6 +165,7 @@ def lbfgsb_minimize(obj, lo=None, hi=None, maxiter: int = 100, m: int = 10,
     n = obj.n_local
     dev = obj.device
     lo, hi = _box(lo, hi, n, dev)
+    lo64, hi64 = lo.double(), hi.double()
     x = torch.minimum(torch.maximum(obj.x0().contiguous(), lo), hi)
     f, g = obj(x)
     g = g.clone()
@@ -192,7 +193,7 @@ def lbfgsb_minimize(obj, lo=None, hi=None, maxiter: int = 100, m: int = 10,
         free_path = t > 0
         d = torch.where(free_path, -g, torch.zeros_like(g))
         xd = x.double()
-        pg = (torch.minimum(torch.maximum(xd - g.double(), lo.double()), hi.double()) - xd).abs()
+        pg = (torch.minimum(torch.maximum(xd - g.double(), lo64), hi64) - xd).abs()
         vecs = [d] if pending is None else [H.s(pending), H.y(pending), d]
         dots_dev = dot(H.HS, 2 * R, vecs)
         tc = torch.where(free_path & torch.isfinite(t), t, torch.full_like(t, math.inf))
@@ -239,9 +240,11 @@ def lbfgsb_minimize(obj, lo=None, hi=None, maxiter: int = 100, m: int = 10,
         rF = torch.where(free, r, torch.zeros_like(r))
         act = torch.nonzero(~free).reshape(-1)
         WtZr = dot(H.HS, 2 * R, [rF])[:, 0]
-        WA = H.HS[torch.as_tensor(rows, device=dev)][:, act].double() if kk2 else \
-            torch.zeros((0, act.numel()), dtype=torch.float64, device=dev)
-        GA = WA @ WA.T
+        if kk2:
+            rows_d = torch.as_tensor(rows, device=dev)
+            GA = _gram(H.HS[rows_d[:, None], act[None, :]].double())
+        else:
+            GA = torch.zeros((0, 0), dtype=torch.float64, device=dev)
         packB = torch.cat([WtZr.reshape(-1), GA.reshape(-1)]).cpu().numpy()
         redB = allsum(packB)
         WtZr_np = redB[:2 * R]
@@ -354,13 +357,17 @@ def _cauchy_point(dd, p0, M, theta, tc, nfin, g, HS, rows, fac, comm, K):
     rows_t = torch.as_tensor(rows, dtype=torch.int64, device=dev)
     fac_t = torch.as_tensor(fac, dtype=torch.float64, device=dev)
     multi = comm is not None and comm.size > 1
-    B = int(K) if K is not None else (1 << 16 if multi else 1 << 20)
+    # batch sizes: K if given, else geometric from 2^14 (the Cauchy point usually lies among
+    # the first few thousand breakpoints, and a scan costs O(2k x batch) in fp64) up to
+    # 2^16 per rank (several ranks: one all-gather per batch) or 2^20 (one rank)
+    B_cap = int(K) if K is not None else (1 << 16 if multi else 1 << 20)
+    B = int(K) if K is not None else min(1 << 14, B_cap)
     ptr = 0
     while True:
         sel = order[ptr:ptr + B]
         tb = tc[sel].double()
         gb = g[sel].double()
-        Wb = (HS[rows_t][:, sel].double() * fac_t[:, None]) if k2 else \
+        Wb = (HS[rows_t[:, None], sel[None, :]].double() * fac_t[:, None]) if k2 else \
             torch.zeros((0, sel.numel()), dtype=torch.float64, device=dev)
         left = nfin - ptr  # this rank's finite breakpoints not yet scanned
         if multi:
@@ -393,11 +400,38 @@ def _cauchy_point(dd, p0, M, theta, tc, nfin, g, HS, rows, fac, comm, K):
         if found:
             return tstar, c.cpu().numpy()
         ptr += mine_used
+        B = min(B * 8, B_cap)
         if not more:
             dtmin = -st["fp"] / st["fpp"] if st["fpp"] > 0 else 0.0
             dtmin = max(dtmin, 0.0)
             c = st["c"] + dtmin * st["p"]
             return st["told"] + dtmin, c.cpu().numpy()
+
+
+def _rowcumsum(X: torch.Tensor) -> torch.Tensor:
+    """Inclusive cumulative sum along the last dim of a (R x N) tensor as ONE device-wide
+    scan of the flattened data minus each row's start offset.  torch's per-row scan runs
+    one block per row, so with R = 2k ~ 20 rows it used ~20 blocks of the GPU (565 us per
+    call at N = 2^20, against ~0.1 ms here); fp64, so the offsets cost no accuracy."""
+    if X.dim() == 1 or X.shape[0] == 1:
+        return torch.cumsum(X, -1)
+    c = torch.cumsum(X.reshape(-1), 0).reshape(X.shape)
+    off = torch.cat([torch.zeros(1, dtype=c.dtype, device=c.device), c[:-1, -1]])
+    return c - off[:, None]
+
+
+def _gram(A: torch.Tensor, chunk: int = 8192) -> torch.Tensor:
+    """``A @ A.T`` for a short, very wide fp64 ``A`` (2k x K): a batched product over column
+    chunks, summed.  A single GEMM with M = N = 2k and K ~ 1e6-1e7 runs a 128x128 tile
+    with no split of K (5.4 ms measured at K ~ 5e6)."""
+    R, K = A.shape
+    if K <= 4 * chunk:
+        return A @ A.T
+    nc = -(-K // chunk)
+    Ap = torch.zeros((R, nc * chunk), dtype=A.dtype, device=A.device)
+    Ap[:, :K] = A
+    X = Ap.view(R, nc, chunk).permute(1, 0, 2)          # (nc, R, chunk), strided view
+    return torch.bmm(X, X.transpose(1, 2)).sum(0)
 
 
 def _scan_batch(st, t, g, W, M, theta):
@@ -413,13 +447,13 @@ def _scan_batch(st, t, g, W, M, theta):
     prev = torch.cat([torch.full((1,), told0, dtype=torch.float64, device=t.device), t[:-1]])
     dt = t - prev
     gw = W * g[None, :]
-    P = st["p"][:, None] + torch.cumsum(gw, 1) - gw          # p before breakpoint i
+    P = st["p"][:, None] + _rowcumsum(gw) - gw               # p before breakpoint i
     Mw = M @ W                                               # M w_i (M symmetric)
     wMp = (Mw * P).sum(0)
     wMw = (Mw * W).sum(0)
     dfpp = -theta * g * g - 2 * g * wMp - g * g * wMw
     fpp_b = st["fpp"] + torch.cumsum(dfpp, 0) - dfpp          # f'' at the start of segment i
-    Cp = st["c"][:, None] + torch.cumsum(P * dt[None, :], 1)  # c after breakpoint i
+    Cp = st["c"][:, None] + _rowcumsum(P * dt[None, :])     # c after breakpoint i
     wMc = (Mw * Cp).sum(0)
     dfp = dt * fpp_b + g * g - theta * t * g * g - g * wMc
     fp_b = st["fp"] + torch.cumsum(dfp, 0) - dfp              # f' at the start of segment i
