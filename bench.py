@@ -167,6 +167,7 @@ def time_placement(placement, args, comm, dev, sync):
         "setup_s": round(setup_s, 2),
         "history": history,
         "device_ops_per_step": ops or None,
+        "overlap": getattr(engine, "overlap_tuning", None),
     }
     if args.profile_phases:
         info["phases_ms"] = {k: round(v, 4) for k, v in engine.timer.summary().items()}
@@ -244,6 +245,7 @@ def main(argv=None):
             "chunks": head["chunks"],
             "layout": head["layout"],
             "device_ops_per_step": head["device_ops_per_step"],
+            "exchange_overlap": head["overlap"],
         },
         "owner_steps_per_s": None if own is None else round(own["steps_per_s"], 3),
         "owner_ms_per_step": None if own is None else round(own["ms_per_step"], 4),

@@ -283,7 +283,8 @@ void xgmi_twoshot(std::vector<int64_t> gbufs, std::vector<int64_t> tbufs, std::v
   TORCH_CHECK(lo >= 0 && n >= 0 && lo % 4 == 0 && n % 4 == 0 && lo + n <= total,
               "owned range must be float4 aligned and inside the vector");
   TORCH_CHECK(mode >= 0 && mode <= 3, "bad mode");
-  TORCH_CHECK(scalars.size() == 7, "scalars: host_step, lr, b1, b2, eps, timeout_s, traj_stride");
+  TORCH_CHECK(scalars.size() == 7 || scalars.size() == 8,
+              "scalars: host_step, lr, b1, b2, eps, timeout_s, traj_stride[, max_blocks]");
   TORCH_CHECK(step.is_cuda() && step.scalar_type() == at::kInt && step.numel() >= 2, "step: [2] int32 device");
   TORCH_CHECK(seq.is_cuda() && seq.scalar_type() == at::kInt && err.is_cuda() && err.scalar_type() == at::kInt,
               "seq/err: int32 device");
@@ -321,7 +322,10 @@ void xgmi_twoshot(std::vector<int64_t> gbufs, std::vector<int64_t> tbufs, std::v
   a.seq = reinterpret_cast<unsigned*>(seq.data_ptr<int>());
   a.err = err.data_ptr<int>();
   const int64_t n4 = n / 4;
-  const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((n4 + kTsThreads - 1) / kTsThreads, 1024));
+  // grid cap: 1024 by default; a smaller cap (scalars[7]) leaves the CUs to the compute
+  // kernels an exchange on a side stream overlaps (the grid-stride loop covers any size)
+  const int64_t cap = scalars.size() == 8 && scalars[7] >= 1 ? std::min<int64_t>((int64_t)scalars[7], 1024) : 1024;
+  const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((n4 + kTsThreads - 1) / kTsThreads, cap));
   auto stream = at::hip::getCurrentHIPStream();
   switch (mode) {
     case 0: hipLaunchKernelGGL(xgmi_twoshot_kernel<0>, dim3(blocks), dim3(kTsThreads), 0, stream, a); break;

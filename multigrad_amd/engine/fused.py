@@ -52,6 +52,7 @@ from __future__ import annotations
 
 import math
 import os
+import time
 from typing import List, Optional
 
 import torch
@@ -71,6 +72,16 @@ def _env_flag(name: str, default: Optional[bool]) -> Optional[bool]:
     if v is None:
         return default
     return v.lower() not in ("0", "false", "off", "no")
+
+
+def _side_stream_mode() -> str:
+    """``MULTIGRAD_TWOSHOT_SIDE_STREAM``: 1/on, 0/off, unset/auto (measured at setup)."""
+    v = os.environ.get("MULTIGRAD_TWOSHOT_SIDE_STREAM", "auto").strip().lower()
+    if v in ("1", "on", "true", "yes"):
+        return "on"
+    if v in ("0", "off", "false", "no"):
+        return "off"
+    return "auto"
 
 
 def plan_chunks(J: int, upp: int, world: int, nchunks: int):
@@ -174,10 +185,10 @@ class FusedAdamEngine:
             W = self.size if self.zero else 1
             self.twoshot = None
             if self.zero and dev.type == "cuda":
-                # two-shot: one chunk by default -- each extra chunk is one more cross-rank
-                # rendezvous per step, and overlapping chunks needs a side stream whose
-                # event waits measured ~100 us per step (profiles/twoshot_2rank.md)
-                nch = self.nchunks_req if self._chunks_explicit else 1
+                # two-shot: 2 chunks by default when the overlapped schedule may be chosen
+                # (side stream auto), else 1 -- each chunk is one more cross-rank rendezvous
+                side_mode = _side_stream_mode()
+                nch = self.nchunks_req if self._chunks_explicit else (2 if side_mode == "auto" else 1)
                 ub, pb, P_pad, lengths = plan_chunks(J, upp, W, nch)
                 self.twoshot = self._connect_twoshot(P_pad)  # collective
             if self.twoshot is None:
@@ -299,15 +310,22 @@ class FusedAdamEngine:
                 self.comm_ag = self.comm.split(0)
         self._ag: List = [None] * self.C
         self.comm_stream = None
-        if self.twoshot is not None and _env_flag("MULTIGRAD_TWOSHOT_SIDE_STREAM", False):
-            # opt-in: the two-shot exchange of chunk c runs on a side stream as soon as the
-            # VJP of chunk c is done (overlapping the VJP of chunk c+1), and the next
-            # step's forward of chunk c waits only for that chunk's exchange.  Off by
-            # default: the cross-stream event waits cost more than the overlap gains on
-            # this stack (profiles/twoshot_2rank.md)
+        self.ts_side = False
+        self.overlap_tuning = None
+        side_mode = _side_stream_mode()
+        if self.twoshot is not None and self.C > 1 and side_mode != "off":
+            # overlapped schedule: the two-shot exchange of chunk c runs on a side stream as
+            # soon as the VJP of chunk c is done (overlapping the VJP of chunk c+1), and the
+            # next step's forward of chunk c waits only for that chunk's exchange; its grid
+            # is capped so the compute kernels keep most CUs.  "auto" (default) times both
+            # schedules on this machine at setup (_tune_overlap) and keeps the faster: with
+            # two ranks sharing one GPU the side stream only adds event waits, across xGMI
+            # it hides part of the exchange behind compute.
             self.comm_stream = torch.cuda.Stream(device=dev)
+            self.ts_blocks = int(os.environ.get("MULTIGRAD_TWOSHOT_BLOCKS", "256"))
             self.ev_vjp = [torch.cuda.Event() for _ in range(self.C)]
             self.ev_ts = [torch.cuda.Event() for _ in range(self.C)]
+            self.ts_side = side_mode == "on"
         self._ts_pending = [False] * self.C
         self.pending = False
         ok = getattr(md, "engine_pipeline_ok", None)
@@ -321,7 +339,7 @@ class FusedAdamEngine:
         # RCCL/gloo calls are not captured
         self.capturable = dev.type == "cuda" and (
             self.size == 1 or (self.oneshot is not None and self.fuse_epilogue and
-                               (self.owner or (self.twoshot is not None and self.comm_stream is None))))
+                               (self.owner or (self.twoshot is not None and not self.ts_side))))
         if self._graph_auto:
             # a pipelined step is two launches (forward+update, epilogue); replaying them
             # from a graph measured 1-5% slower than eager launches (tools/graph_ab_full.sh).
@@ -333,7 +351,47 @@ class FusedAdamEngine:
             self.use_graph = False  # e.g. RCCL collectives in the step: eager launches
         self.graph = None
         self.ready = True
+        if self.comm_stream is not None and side_mode == "auto" and not self.use_graph:
+            self._tune_overlap()
         return self
+
+    def _tune_overlap(self, reps: int = 3):
+        """Collective: time ``reps`` steps with the chunk exchanges on the compute stream and
+        ``reps`` with them on the side stream (after one warm-up step each, syncs only at
+        the window edges), keep the schedule whose slowest rank was faster, then restore
+        the optimizer state -- the trajectory is unaffected."""
+        saved = [t.clone() for t in (self.theta, self.m, self.v, self.step_dev)]
+        u_saved = self.u_loc.clone() if self.u_loc is not None else None
+        times = {}
+        for side in (False, True):
+            self.ts_side = side
+            self._enqueue_step()
+            self._drain_all()
+            torch.cuda.synchronize()
+            self.comm.barrier()
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                self._enqueue_step()
+            self._drain_all()
+            torch.cuda.synchronize()
+            dt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+            self.comm.all_reduce(dt, op="max")
+            times[side] = float(dt) / reps
+        self.check("overlap tuning", collective=True)
+        for t, v in zip((self.theta, self.m, self.v, self.step_dev), saved):
+            t.copy_(v)
+        if u_saved is not None:
+            self.u_loc.copy_(u_saved)
+        self.ts_side = times[True] < times[False]
+        self.overlap_tuning = {"same_stream_ms": round(1e3 * times[False], 4),
+                               "side_stream_ms": round(1e3 * times[True], 4),
+                               "side_stream": self.ts_side}
+        torch.cuda.synchronize()
+        self.comm.barrier()
+
+    def _drain_all(self):
+        for c in range(self.C):
+            self._drain(c)
 
     # ------------------------------------------------------------------ helpers
     def _connect_twoshot(self, numel: int):
@@ -354,7 +412,7 @@ class FusedAdamEngine:
     def _twoshot_update(self, c: int):
         """Chunk c: dense-gradient reduce-scatter + Adam on the owned slice + all-gather,
         one launch on the side stream after the chunk's VJP."""
-        side = self.comm_stream is not None
+        side = self.ts_side
         if side:
             self.ev_vjp[c].record(torch.cuda.current_stream())
             self.comm_stream.wait_event(self.ev_vjp[c])
@@ -369,7 +427,8 @@ class FusedAdamEngine:
                               bounds=bnd, traj=traj,
                               traj_stride=0 if traj is None else self.traj_loc.shape[1],
                               step=self.step_dev[c], host_step=self._hstep(), lr=self.lr,
-                              b1=self.b1, b2=self.b2, eps=self.eps)
+                              b1=self.b1, b2=self.b2, eps=self.eps,
+                              max_blocks=self.ts_blocks if side else 0)
         if side:
             self.ev_ts[c].record(self.comm_stream)
             self._ts_pending[c] = True
@@ -716,7 +775,10 @@ class FusedAdamEngine:
         if self.owner:
             return "none: owner-local gradients, sumstat all-reduce only"
         if self.zero and self.twoshot is not None:
-            return "xGMI two-shot kernel: reduce-scatter + Adam + all-gather in one launch (self-tested)"
+            sched = (f", {self.C} chunks on a side stream overlapping compute" if self.ts_side
+                     else f", {self.C} chunk(s) on the compute stream")
+            return ("xGMI two-shot kernel: reduce-scatter + Adam + all-gather in one launch per "
+                    "chunk (self-tested)" + sched)
         if self.zero:
             return "RCCL reduce-scatter + all-gather (ZeRO-1)"
         return "RCCL all-reduce"

@@ -35,7 +35,7 @@ import torch
 
 __all__ = ["OneShotAllReduce", "CollectiveTimeout", "oneshot_enabled", "oneshot_mode",
            "connect", "get_oneshot", "maybe_oneshot", "MAX_FLOATS", "MAX_RANKS", "TwoShot",
-           "connect_twoshot", "twoshot_enabled"]
+           "connect_twoshot", "twoshot_enabled", "get_twoshot_allreduce"]
 
 MAX_FLOATS = 64
 MAX_RANKS = 8
@@ -269,9 +269,10 @@ class TwoShot:
     def step(self, lo: int, n: int, mode: int, m=None, v=None, u=None, bounds=None, traj=None,
              traj_stride: int = 0, step: Optional[torch.Tensor] = None,
              host_step: Optional[int] = None, lr: float = 0.0, b1: float = 0.9, b2: float = 0.999,
-             eps: float = 1e-8) -> None:
+             eps: float = 1e-8, max_blocks: int = 0) -> None:
         """Enqueue one exchange on the current stream.  ``mode`` 0: theta = sum of the
-        gradients (self-test); 1: unbounded Adam; 2/3: bounded (3: legacy Jacobian)."""
+        gradients (self-test); 1: unbounded Adam; 2/3: bounded (3: legacy Jacobian).
+        ``max_blocks`` caps the grid (0: the default 1024)."""
         from ..ops._ext import ext
         lo_b = hi_b = kind = None
         if bounds is not None:
@@ -280,7 +281,8 @@ class TwoShot:
                            self.numel, int(mode), u, m, v, lo_b, hi_b, kind, traj,
                            self._step0 if step is None else step, self.seq, self.err,
                            [float(-1 if host_step is None else host_step), float(lr), float(b1),
-                            float(b2), float(eps), self.timeout_s, float(traj_stride)])
+                            float(b2), float(eps), self.timeout_s, float(traj_stride),
+                            float(max_blocks)])
 
     def check(self, where: str = "", comm=None) -> None:
         OneShotAllReduce.check(self, where, comm)  # same err/seq protocol words

@@ -126,10 +126,11 @@ def test_twoshot_adam_modes_match_reference():
         np.testing.assert_array_equal(out[0][0][mode][0], out[1][0][mode][0])
 
 
-def _engine_hashed(rank, size, twoshot, bounded, chunks, layout="auto", graph=None):
+def _engine_hashed(rank, size, twoshot, bounded, chunks, layout="auto", graph=None, side="auto"):
     lane_order = "local" if layout == "lanes" else None
     if graph is not None:
         os.environ["MULTIGRAD_GRAPH"] = "1" if graph else "0"
+    os.environ["MULTIGRAD_TWOSHOT_SIDE_STREAM"] = side
     os.environ["MULTIGRAD_TWOSHOT"] = "1" if twoshot else "0"
     os.environ["MULTIGRAD_CHUNKS"] = str(chunks)
     import multigrad_amd as mg
@@ -151,22 +152,32 @@ def _engine_hashed(rank, size, twoshot, bounded, chunks, layout="auto", graph=No
     sh = data["shard"]
     return (traj.cpu().numpy(), eng.twoshot is not None, eng.zero,
             f"{sh.layout}/{sh.lane_order}" if sh.layout == "lanes" else sh.layout,
-            eng.grad_collective_name(), eng.C, eng.use_graph and eng.graph is not None)
+            eng.grad_collective_name(), eng.C, eng.use_graph and eng.graph is not None,
+            eng.ts_side, eng.overlap_tuning)
 
 
-@pytest.mark.parametrize("bounded,chunks,layout", [(False, 1, "auto"), (True, 1, "auto"),
-                                                   (False, 3, "auto"), (True, 4, "auto"),
-                                                   (False, 2, "lanes")])
-def test_engine_hashed_twoshot_matches_rccl_path(bounded, chunks, layout):
-    """One chunk, and several chunks whose exchanges run on the side stream overlapping
-    the next chunk's VJP and the next step's forward: same bits as the RCCL/gloo path
-    (the auto layout = tiles for hashed shards, and lanes in the local slot order with the
-    recomputing VJP)."""
-    ref = run_distributed(_engine_hashed, 2, False, bounded, chunks, layout, timeout=600)
-    res = run_distributed(_engine_hashed, 2, True, bounded, chunks, layout, timeout=600)
+@pytest.mark.parametrize("bounded,chunks,layout,side", [
+    (False, 1, "auto", "auto"), (True, 1, "auto", "auto"), (False, 3, "auto", "on"),
+    (True, 4, "auto", "on"), (False, 3, "auto", "off"), (True, 2, "auto", "auto"),
+    (False, 2, "lanes", "on")])
+def test_engine_hashed_twoshot_matches_rccl_path(bounded, chunks, layout, side):
+    """One chunk, and several chunks whose exchanges run on the compute stream ("off"), on
+    the side stream overlapping the next chunk's VJP and the next step's forward ("on"),
+    or whichever the setup-time timing picked ("auto": the timing steps are undone): same
+    bits as the RCCL/gloo path (the auto layout = tiles for hashed shards, and lanes in the
+    local slot order with the recomputing VJP)."""
+    ref = run_distributed(_engine_hashed, 2, False, bounded, chunks, layout, None, side,
+                          timeout=600)
+    res = run_distributed(_engine_hashed, 2, True, bounded, chunks, layout, None, side,
+                          timeout=600)
     want = "tiles" if layout == "auto" else "lanes/local"
     assert all(r[2] and r[3] == want and r[5] == chunks for r in ref + res), ref[0][3]
     assert not ref[0][1] and res[0][1] and res[1][1], (ref[0][4], res[0][4])
+    if chunks > 1:
+        assert res[0][7] == res[1][7] and (res[0][7] if side == "on" else True)
+        assert (res[0][8] is not None) == (side == "auto"), res[0][8]
+        if side == "off":
+            assert not res[0][7]
     np.testing.assert_array_equal(res[0][0], res[1][0])
     np.testing.assert_array_equal(ref[0][0], ref[1][0])
     np.testing.assert_array_equal(res[0][0], ref[0][0])  # bitwise: same sums, same Adam bits
