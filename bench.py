@@ -168,6 +168,7 @@ def time_placement(placement, args, comm, dev, sync):
         "history": history,
         "device_ops_per_step": ops or None,
         "overlap": getattr(engine, "overlap_tuning", None),
+        "graph_tuning": getattr(engine, "graph_tuning", None),
     }
     if args.profile_phases:
         info["phases_ms"] = {k: round(v, 4) for k, v in engine.timer.summary().items()}
@@ -246,6 +247,7 @@ def main(argv=None):
             "layout": head["layout"],
             "device_ops_per_step": head["device_ops_per_step"],
             "exchange_overlap": head["overlap"],
+            "graph_tuning": head["graph_tuning"],
         },
         "owner_steps_per_s": None if own is None else round(own["steps_per_s"], 3),
         "owner_ms_per_step": None if own is None else round(own["ms_per_step"], 4),

@@ -350,9 +350,13 @@ class FusedAdamEngine:
         elif self.use_graph and not self.capturable:
             self.use_graph = False  # e.g. RCCL collectives in the step: eager launches
         self.graph = None
+        self.graph_tuning = None
         self.ready = True
         if self.comm_stream is not None and side_mode == "auto" and not self.use_graph:
             self._tune_overlap()
+        if self._graph_auto and self.capturable and self.size == 1 and \
+                _env_flag("MULTIGRAD_GRAPH_TUNE", True):
+            self._tune_graph()
         return self
 
     def _tune_overlap(self, reps: int = 3):
@@ -682,11 +686,7 @@ class FusedAdamEngine:
         finally:
             self._capturing = False
 
-    def step(self):
-        """Enqueue one optimizer step (asynchronous on GPU)."""
-        assert self.ready, "call setup() first"
-        if self.step_host >= self.nsteps and self.history.mode == "full":
-            raise RuntimeError("more steps than the trajectory buffer was sized for")
+    def _raw_step(self):
         if self.use_graph and (self.pending or not self.pipeline):
             if self.graph is None:
                 self._capture()
@@ -696,6 +696,52 @@ class FusedAdamEngine:
         else:
             self._enqueue_step()
         self.step_host += 1
+
+    def _tune_graph(self, warm: int = 4, reps: int = 10):
+        """One rank, auto policy: time ``reps`` eager steps and ``reps`` graph replays (each
+        window after ``warm`` steps, syncs only at its edges), keep the faster, and restore
+        the optimizer state (the trajectory rows it wrote are rewritten by the real steps).
+        The difference is a few percent either way (tools/graph_ab_full.sh); the timing
+        steps also bring the GPU to its working clock before the first real step (a cold
+        start ramps over ~10 ms of work, profiles/step_timeline.md)."""
+        if self.history.mode == "full" and self.nsteps < warm + reps + 1:
+            return  # the timing steps would write past the trajectory buffer
+        state = [self.theta, self.m, self.v, self.step_dev]
+        if getattr(self, "u", None) is not None and self.u is not self.theta:
+            state.append(self.u)
+        saved = [t.clone() for t in state]
+
+        def restore():
+            torch.cuda.synchronize()
+            for t, v in zip(state, saved):
+                t.copy_(v)
+            self.pending = False
+            self.step_host = 0
+
+        times = {}
+        for g in (False, True):
+            self.use_graph = g
+            for _ in range(warm):
+                self._raw_step()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                self._raw_step()
+            torch.cuda.synchronize()
+            times[g] = (time.perf_counter() - t0) / reps
+            restore()
+        self.use_graph = times[True] < times[False]
+        if not self.use_graph:
+            self.graph = None
+        self.graph_tuning = {"eager_ms": round(1e3 * times[False], 4),
+                             "graph_ms": round(1e3 * times[True], 4), "graph": self.use_graph}
+
+    def step(self):
+        """Enqueue one optimizer step (asynchronous on GPU)."""
+        assert self.ready, "call setup() first"
+        if self.step_host >= self.nsteps and self.history.mode == "full":
+            raise RuntimeError("more steps than the trajectory buffer was sized for")
+        self._raw_step()
         if self.history.mode != "full" and self.traj_loc is None:
             if self.pipeline:
                 st = self.history.stride

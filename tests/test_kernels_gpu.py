@@ -380,6 +380,27 @@ def test_pipelined_update_matches_unpipelined(monkeypatch, owner, graph, history
     torch.testing.assert_close(eng.params(), ref[-1], rtol=1e-6, atol=1e-7)
 
 
+@pytest.mark.parametrize("pipeline", ["1", "0"])
+def test_setup_autotune_leaves_trajectory_unchanged(monkeypatch, pipeline):
+    """One rank, auto graph policy: the setup-time eager-vs-replay timing runs steps and
+    restores the state; the trajectory equals a plain eager run's bit for bit (replayed and
+    eager steps launch the same kernels).  Too short a trajectory buffer skips it."""
+    from multigrad_amd.engine.fused import FusedAdamEngine
+    from multigrad_amd.models.population import PopulationSMFModel, make_population_data
+    monkeypatch.setenv("MULTIGRAD_PIPELINE", pipeline)
+    data = make_population_data(num_params=6000, num_halos=300_000, seed=21, device=DEV)
+    model = PopulationSMFModel(aux_data=data)
+    model.set_target_from_truth()
+    ref = FusedAdamEngine(model, graph=False).run_adam(data["guess"], nsteps=16, learning_rate=1e-3)
+    eng = FusedAdamEngine(model)
+    t = eng.run_adam(data["guess"], nsteps=16, learning_rate=1e-3)
+    assert eng.graph_tuning is not None and eng.use_graph == eng.graph_tuning["graph"]
+    torch.testing.assert_close(t, ref, rtol=0, atol=0)
+    short = FusedAdamEngine(model)
+    short.run_adam(data["guess"], nsteps=4, learning_rate=1e-3)
+    assert short.graph_tuning is None
+
+
 @pytest.mark.parametrize("giant", [None, 3])
 def test_lanes_recompute_vjp_matches_residual_vjp(giant):
     """The recomputing lanes VJP (local slot order, hashed shards) against the residual
