@@ -167,8 +167,7 @@ def time_placement(placement, args, comm, dev, sync):
         "setup_s": round(setup_s, 2),
         "history": history,
         "device_ops_per_step": ops or None,
-        "overlap": getattr(engine, "overlap_tuning", None),
-        "graph_tuning": getattr(engine, "graph_tuning", None),
+        "autotune": getattr(engine, "tuning", None),
     }
     if args.profile_phases:
         info["phases_ms"] = {k: round(v, 4) for k, v in engine.timer.summary().items()}
@@ -246,8 +245,7 @@ def main(argv=None):
             "chunks": head["chunks"],
             "layout": head["layout"],
             "device_ops_per_step": head["device_ops_per_step"],
-            "exchange_overlap": head["overlap"],
-            "graph_tuning": head["graph_tuning"],
+            "autotune": head["autotune"],
         },
         "owner_steps_per_s": None if own is None else round(own["steps_per_s"], 3),
         "owner_ms_per_step": None if own is None else round(own["ms_per_step"], 4),
@@ -259,7 +257,7 @@ def main(argv=None):
         rec["owner_config"] = {k: own[k] for k in ("parallelism", "optimizer_sharding",
                                                    "grad_collective", "sumstat_allreduce",
                                                    "chunks", "pipelined", "layout",
-                                                   "device_ops_per_step")}
+                                                   "device_ops_per_step", "autotune", "graph")}
     if args.profile_phases:
         rec["phases_ms"] = head["phases_ms"]
         if own is not None and own is not head:

@@ -311,14 +311,13 @@ class FusedAdamEngine:
         self._ag: List = [None] * self.C
         self.comm_stream = None
         self.ts_side = False
-        self.overlap_tuning = None
         side_mode = _side_stream_mode()
         if self.twoshot is not None and self.C > 1 and side_mode != "off":
             # overlapped schedule: the two-shot exchange of chunk c runs on a side stream as
             # soon as the VJP of chunk c is done (overlapping the VJP of chunk c+1), and the
             # next step's forward of chunk c waits only for that chunk's exchange; its grid
             # is capped so the compute kernels keep most CUs.  "auto" (default) times both
-            # schedules on this machine at setup (_tune_overlap) and keeps the faster: with
+            # schedules on this machine at setup (_autotune) and keeps the faster: with
             # two ranks sharing one GPU the side stream only adds event waits, across xGMI
             # it hides part of the exchange behind compute.
             self.comm_stream = torch.cuda.Stream(device=dev)
@@ -350,48 +349,112 @@ class FusedAdamEngine:
         elif self.use_graph and not self.capturable:
             self.use_graph = False  # e.g. RCCL collectives in the step: eager launches
         self.graph = None
-        self.graph_tuning = None
+        self.tuning = None
+        self._tuning = False
         self.ready = True
+        cands = []
         if self.comm_stream is not None and side_mode == "auto" and not self.use_graph:
-            self._tune_overlap()
-        if self._graph_auto and self.capturable and self.size == 1 and \
-                _env_flag("MULTIGRAD_GRAPH_TUNE", True):
-            self._tune_graph()
+            cands = [{"ts_side": False}, {"ts_side": True}]   # hashed: where the exchange runs
+        elif self._graph_auto and self.capturable and (self.size == 1 or self.owner):
+            cands = [{"use_graph": False}, {"use_graph": True}]  # eager launches vs replay
+        if cands and dev.type == "cuda" and _env_flag("MULTIGRAD_AUTOTUNE", True):
+            self._autotune(cands, min_window_s=1e-3 * float(
+                os.environ.get("MULTIGRAD_AUTOTUNE_WINDOW_MS", "30")))
         return self
 
-    def _tune_overlap(self, reps: int = 3):
-        """Collective: time ``reps`` steps with the chunk exchanges on the compute stream and
-        ``reps`` with them on the side stream (after one warm-up step each, syncs only at
-        the window edges), keep the schedule whose slowest rank was faster, then restore
-        the optimizer state -- the trajectory is unaffected."""
-        saved = [t.clone() for t in (self.theta, self.m, self.v, self.step_dev)]
-        u_saved = self.u_loc.clone() if self.u_loc is not None else None
-        times = {}
-        for side in (False, True):
-            self.ts_side = side
-            self._enqueue_step()
+    # ------------------------------------------------------------------ setup-time tuning
+    def _tl(self):
+        """The sharded trajectory buffer, or None while the autotune steps run."""
+        return None if self._tuning else self.traj_loc
+
+    def _hb(self):
+        """The replicated trajectory buffer (flat), or None (not recorded / autotune)."""
+        if self._tuning or self.history.mode != "full":
+            return None
+        return self.history.buf.reshape(-1)
+
+    def _autotune(self, cands, warm: int = 2, min_window_s: float = 0.008,
+                  max_reps: int = 400):
+        """Collective: time each candidate schedule (a dict of engine attributes) over a
+        window of at least ``min_window_s`` of work after ``warm`` steps, with syncs only
+        at the window edges; keep the candidate whose slowest rank was fastest, then
+        restore the optimizer state.  No trajectory rows are written while tuning, so the
+        recorded trajectory is that of the real steps alone.
+
+        Besides picking the schedule measured fastest on this machine (eager launches vs
+        graph replay; the hashed exchange on the compute or a side stream), the window
+        length brings the GPU to its working clock before the first real step: after a
+        cold start the same step ran 0.88 ms and ~0.64 ms only after ~15 ms of work
+        (profiles/step_timeline.md)."""
+        state = [self.theta, self.m, self.v, self.step_dev]
+        for name in ("u", "u_loc"):
+            t = getattr(self, name, None)
+            if t is not None and all(t is not x for x in state):
+                state.append(t)
+        saved = [t.clone() for t in state]
+        multi = self.size > 1
+
+        def restore():
             self._drain_all()
             torch.cuda.synchronize()
-            self.comm.barrier()
+            for t, v in zip(state, saved):
+                t.copy_(v)
+            self.pending = False
+            self.step_host = 0
+
+        def apply(c):
+            for k, v in c.items():
+                setattr(self, k, v)
+            self.graph = None
+
+        def window(n):
+            self._drain_all()
+            torch.cuda.synchronize()
+            if multi:
+                self.comm.barrier()
             t0 = time.perf_counter()
-            for _ in range(reps):
-                self._enqueue_step()
+            for _ in range(n):
+                self._raw_step()
             self._drain_all()
             torch.cuda.synchronize()
             dt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
-            self.comm.all_reduce(dt, op="max")
-            times[side] = float(dt) / reps
-        self.check("overlap tuning", collective=True)
-        for t, v in zip((self.theta, self.m, self.v, self.step_dev), saved):
-            t.copy_(v)
-        if u_saved is not None:
-            self.u_loc.copy_(u_saved)
-        self.ts_side = times[True] < times[False]
-        self.overlap_tuning = {"same_stream_ms": round(1e3 * times[False], 4),
-                               "side_stream_ms": round(1e3 * times[True], 4),
-                               "side_stream": self.ts_side}
-        torch.cuda.synchronize()
-        self.comm.barrier()
+            if multi:
+                self.comm.all_reduce(dt, op="max")
+            return float(dt) / n
+
+        self._tuning = True
+        try:
+            apply(cands[0])
+            for _ in range(warm):
+                self._raw_step()
+            est = window(2)
+            reps = int(min(max_reps, max(8, math.ceil(min_window_s / max(est, 1e-6)))))
+            restore()
+            times = []
+            for c in cands:
+                apply(c)
+                for _ in range(warm):
+                    self._raw_step()
+                times.append(window(reps))
+                restore()
+            self.check("setup autotune", collective=multi)
+        finally:
+            self._tuning = False
+        best = min(range(len(cands)), key=lambda i: times[i])
+        apply(cands[best])
+        self.tuning = {"candidates": [dict(c, ms=round(1e3 * t, 4)) for c, t in zip(cands, times)],
+                       "chosen": cands[best], "steps_per_window": reps}
+        if self.use_graph:
+            # capture the real (trajectory-writing) step now rather than inside the first
+            # timed step
+            pend = self.pending
+            self.pending = self.pipeline
+            self._capture()
+            self.pending = pend
+        if multi:
+            torch.cuda.synchronize()
+            self.comm.barrier()
+
 
     def _drain_all(self):
         for c in range(self.C):
@@ -424,7 +487,8 @@ class FusedAdamEngine:
         o, n = self.loc_off[c], self.loc_len[c]
         bnd = self._bslice(c)
         mode = 1 if bnd is None else (3 if self.legacy else 2)
-        traj = None if self.traj_loc is None else self.traj_loc.reshape(-1)[o:]
+        tl = self._tl()
+        traj = None if tl is None else tl.reshape(-1)[o:]
         with torch.cuda.stream(self.comm_stream) if side else contextlib.nullcontext():
             self.twoshot.step(a, b - a, mode, m=self.m[o:o + n], v=self.v[o:o + n],
                               u=None if self.u_loc is None else self.u_loc[o:o + n],
@@ -501,10 +565,11 @@ class FusedAdamEngine:
             idx = self.step_host - 1
             if self.owner:
                 a, b = self.own_range
-                tb = None if self.traj_loc is None else self.traj_loc.reshape(-1)
+                tl = self._tl()
+                tb = None if tl is None else tl.reshape(-1)
                 ok = self._fused_vjp_adam(self.rank, a, tb, b - a, host_step=self._hstep(idx))
             else:
-                hb = self.history.buf.reshape(-1) if self.history.mode == "full" else None
+                hb = self._hb()
                 ok = self._fused_vjp_adam(None, 0, hb, self.P if hb is not None else 0,
                                           host_step=self._hstep(idx))
             assert ok, "pipelined engine lost its fused VJP + Adam path"
@@ -514,11 +579,12 @@ class FusedAdamEngine:
         """Arguments of the pending (pipelined) VJP + Adam of step ``step_idx``."""
         if self.owner:
             a, b = self.own_range
-            traj = None if self.traj_loc is None else self.traj_loc.reshape(-1)
+            tl = self._tl()
+            traj = None if tl is None else tl.reshape(-1)
             stride = b - a
         else:
             a = 0
-            traj = self.history.buf.reshape(-1) if self.history.mode == "full" else None
+            traj = self._hb()
             stride = self.P
         return dict(h=self.h, m=self.m, v=self.v, unit_offset=a // self.upp,
                     step=self.step_dev[0], host_step=self._hstep(step_idx), lr=self.lr,
@@ -569,10 +635,10 @@ class FusedAdamEngine:
             self.pending = True
             return
         self._forward_loss()
-        hb = self.history.buf.reshape(-1) if self.history.mode == "full" else None
+        hb = self._hb()
+        tl = self._tl()
         if self.owner and self._fused_vjp_adam(self.rank, self.own_range[0],
-                                               None if self.traj_loc is None
-                                               else self.traj_loc.reshape(-1),
+                                               None if tl is None else tl.reshape(-1),
                                                self.own_range[1] - self.own_range[0]):
             pass
         elif self.owner:
@@ -582,7 +648,7 @@ class FusedAdamEngine:
             a, b = self.own_range
             u = self.u_loc if self.u_loc is not None else self.theta[a:b]
             p = self.theta[a:b] if self.u_loc is not None else None
-            tb = None if self.traj_loc is None else self.traj_loc.reshape(-1)
+            tb = None if tl is None else tl.reshape(-1)
             with self._ph("adam"):
                 adam_step_(u, self.m, self.v, self.grad[a:b], p, self.step_dev[0], self.lr,
                            self.b1, self.b2, self.eps, self.bounds_loc, self.legacy,
@@ -609,7 +675,7 @@ class FusedAdamEngine:
                 o, n = self.loc_off[c], self.loc_len[c]
                 u = self.u_loc[o:o + n] if self.u_loc is not None else self.theta[a:b]
                 p = self.theta[a:b] if self.u_loc is not None else None
-                tb = None if self.traj_loc is None else self.traj_loc.reshape(-1)[o:]
+                tb = None if tl is None else tl.reshape(-1)[o:]
                 with self._ph("adam"):
                     adam_step_(u, self.m[o:o + n], self.v[o:o + n], self.g_loc[o:o + n], p,
                                self.step_dev[c], self.lr, self.b1, self.b2, self.eps,
@@ -696,45 +762,6 @@ class FusedAdamEngine:
         else:
             self._enqueue_step()
         self.step_host += 1
-
-    def _tune_graph(self, warm: int = 4, reps: int = 10):
-        """One rank, auto policy: time ``reps`` eager steps and ``reps`` graph replays (each
-        window after ``warm`` steps, syncs only at its edges), keep the faster, and restore
-        the optimizer state (the trajectory rows it wrote are rewritten by the real steps).
-        The difference is a few percent either way (tools/graph_ab_full.sh); the timing
-        steps also bring the GPU to its working clock before the first real step (a cold
-        start ramps over ~10 ms of work, profiles/step_timeline.md)."""
-        if self.history.mode == "full" and self.nsteps < warm + reps + 1:
-            return  # the timing steps would write past the trajectory buffer
-        state = [self.theta, self.m, self.v, self.step_dev]
-        if getattr(self, "u", None) is not None and self.u is not self.theta:
-            state.append(self.u)
-        saved = [t.clone() for t in state]
-
-        def restore():
-            torch.cuda.synchronize()
-            for t, v in zip(state, saved):
-                t.copy_(v)
-            self.pending = False
-            self.step_host = 0
-
-        times = {}
-        for g in (False, True):
-            self.use_graph = g
-            for _ in range(warm):
-                self._raw_step()
-            torch.cuda.synchronize()
-            t0 = time.perf_counter()
-            for _ in range(reps):
-                self._raw_step()
-            torch.cuda.synchronize()
-            times[g] = (time.perf_counter() - t0) / reps
-            restore()
-        self.use_graph = times[True] < times[False]
-        if not self.use_graph:
-            self.graph = None
-        self.graph_tuning = {"eager_ms": round(1e3 * times[False], 4),
-                             "graph_ms": round(1e3 * times[True], 4), "graph": self.use_graph}
 
     def step(self):
         """Enqueue one optimizer step (asynchronous on GPU)."""

@@ -382,23 +382,26 @@ def test_pipelined_update_matches_unpipelined(monkeypatch, owner, graph, history
 
 @pytest.mark.parametrize("pipeline", ["1", "0"])
 def test_setup_autotune_leaves_trajectory_unchanged(monkeypatch, pipeline):
-    """One rank, auto graph policy: the setup-time eager-vs-replay timing runs steps and
-    restores the state; the trajectory equals a plain eager run's bit for bit (replayed and
-    eager steps launch the same kernels).  Too short a trajectory buffer skips it."""
+    """One rank, auto graph policy: the setup-time eager-vs-replay timing runs steps (no
+    trajectory rows) and restores the state; the trajectory equals a plain eager run's bit
+    for bit (replayed and eager steps launch the same kernels), even when it is shorter
+    than the tuning windows."""
     from multigrad_amd.engine.fused import FusedAdamEngine
     from multigrad_amd.models.population import PopulationSMFModel, make_population_data
     monkeypatch.setenv("MULTIGRAD_PIPELINE", pipeline)
     data = make_population_data(num_params=6000, num_halos=300_000, seed=21, device=DEV)
     model = PopulationSMFModel(aux_data=data)
     model.set_target_from_truth()
-    ref = FusedAdamEngine(model, graph=False).run_adam(data["guess"], nsteps=16, learning_rate=1e-3)
+    ref = FusedAdamEngine(model, graph=False).run_adam(data["guess"], nsteps=6, learning_rate=1e-3)
     eng = FusedAdamEngine(model)
-    t = eng.run_adam(data["guess"], nsteps=16, learning_rate=1e-3)
-    assert eng.graph_tuning is not None and eng.use_graph == eng.graph_tuning["graph"]
+    t = eng.run_adam(data["guess"], nsteps=6, learning_rate=1e-3)
+    assert eng.tuning is not None and eng.use_graph == eng.tuning["chosen"]["use_graph"]
+    assert eng.tuning["steps_per_window"] >= 8
     torch.testing.assert_close(t, ref, rtol=0, atol=0)
-    short = FusedAdamEngine(model)
-    short.run_adam(data["guess"], nsteps=4, learning_rate=1e-3)
-    assert short.graph_tuning is None
+    monkeypatch.setenv("MULTIGRAD_AUTOTUNE", "0")
+    off = FusedAdamEngine(model)
+    off.setup(data["guess"], 4, learning_rate=1e-3)
+    assert off.tuning is None
 
 
 @pytest.mark.parametrize("giant", [None, 3])

@@ -153,7 +153,7 @@ def _engine_hashed(rank, size, twoshot, bounded, chunks, layout="auto", graph=No
     return (traj.cpu().numpy(), eng.twoshot is not None, eng.zero,
             f"{sh.layout}/{sh.lane_order}" if sh.layout == "lanes" else sh.layout,
             eng.grad_collective_name(), eng.C, eng.use_graph and eng.graph is not None,
-            eng.ts_side, eng.overlap_tuning)
+            eng.ts_side, eng.tuning)
 
 
 @pytest.mark.parametrize("bounded,chunks,layout,side", [

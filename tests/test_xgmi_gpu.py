@@ -56,9 +56,11 @@ def test_oneshot_protocol_two_procs_one_gpu():
         np.testing.assert_array_equal(y, x)
 
 
-def _engine(rank, size, oneshot):
+def _engine(rank, size, oneshot, graph=None):
     import os
     os.environ["MULTIGRAD_ALLREDUCE"] = "oneshot" if oneshot else "rccl"
+    if graph is not None:
+        os.environ["MULTIGRAD_GRAPH"] = "1" if graph else "0"
     import multigrad_amd as mg
     from multigrad_amd.engine.fused import FusedAdamEngine
     from multigrad_amd.models.population import PopulationSMFModel, make_population_data
@@ -70,7 +72,21 @@ def _engine(rank, size, oneshot):
     eng = FusedAdamEngine(model)
     traj = eng.run_adam(data["guess"], nsteps=6, learning_rate=1e-3)
     used = bool(getattr(comm, "_oneshot", None))
-    return traj.cpu().numpy(), used
+    return traj.cpu().numpy(), used, bool(eng.use_graph and eng.graph is not None), eng.tuning
+
+
+def test_owner_engine_graph_replay_matches_eager():
+    """Owner placement, two ranks: the pipelined step (forward + fused update, one-shot
+    epilogue) replayed from a HIP graph on every rank gives the eager trajectory bit for
+    bit; the auto policy (setup-time timing of both, state restored) does too."""
+    eager = run_distributed(_engine, 2, True, False, timeout=600)
+    graph = run_distributed(_engine, 2, True, True, timeout=600)
+    auto = run_distributed(_engine, 2, True, None, timeout=600)
+    assert not eager[0][2] and graph[0][2] and graph[1][2]
+    assert auto[0][3] is not None and auto[0][3]["chosen"] == auto[1][3]["chosen"]
+    for r in range(2):
+        np.testing.assert_array_equal(graph[r][0], eager[r][0])
+        np.testing.assert_array_equal(auto[r][0], eager[r][0])
 
 
 def test_engine_with_oneshot_sumstat_allreduce():
