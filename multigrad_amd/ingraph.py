@@ -17,7 +17,6 @@ all-reduced update.
 """
 from __future__ import annotations
 
-import math
 from typing import Callable
 
 import torch

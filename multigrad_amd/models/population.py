@@ -17,7 +17,6 @@ scaling: the total data is independent of the number of GPUs), on its own GPU.
 """
 from __future__ import annotations
 
-import math
 from dataclasses import dataclass
 from typing import Optional
 

@@ -14,8 +14,8 @@ sumstats are partition invariant.
 """
 from __future__ import annotations
 
-from dataclasses import dataclass, field
-from typing import Any, NamedTuple, Optional
+from dataclasses import dataclass
+from typing import NamedTuple
 
 import numpy as np
 import torch

@@ -1,9 +1,8 @@
 """L-BFGS vector ops (``csrc/lbfgs.hip``) with PyTorch fallbacks for CPU tensors."""
 from __future__ import annotations
 
-from typing import List, Optional, Sequence
+from typing import Optional, Sequence
 
-import numpy as np
 import torch
 
 from ._ext import ext

@@ -22,7 +22,7 @@ from __future__ import annotations
 
 import math
 import os
-from typing import Any, Callable, Optional
+from typing import Callable, Optional
 
 import torch
 

@@ -27,7 +27,7 @@ from __future__ import annotations
 
 import math
 import os
-from typing import Callable, Optional
+from typing import Callable
 
 import numpy as np
 import scipy.linalg

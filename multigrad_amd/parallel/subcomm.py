@@ -20,7 +20,7 @@ from typing import Optional, Tuple
 import numpy as np
 import torch
 
-from .comm import Comm, SerialComm, get_world_comm, processor_name
+from .comm import Comm, get_world_comm, processor_name
 
 __all__ = ["reduce_sum", "split_subcomms", "split_subcomms_by_node", "scatter_nd",
            "distribute_data"]
