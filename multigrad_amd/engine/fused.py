@@ -856,6 +856,18 @@ class FusedAdamEngine:
             return "RCCL reduce-scatter + all-gather (ZeRO-1)"
         return "RCCL all-reduce"
 
+    def comm_bytes_per_step(self) -> int:
+        """Bytes this rank sends through collectives in one step: the sumstat exchange,
+        plus the dense-gradient exchange of the hashed placement (reduce-scatter and
+        parameter all-gather, or an all-reduce: 2 (W-1)/W of the vector either way)."""
+        W = self.size
+        if W == 1:
+            return 0
+        nbytes = 4 * self.nS * (W - 1)  # one-shot push (RCCL moves about as much)
+        if not self.owner:
+            nbytes += int(2 * (W - 1) * (self.P_pad // W) * 4)
+        return nbytes
+
     def sumstat_collective_name(self) -> str:
         if self.size == 1:
             return "none (1 rank)"
@@ -979,10 +991,11 @@ class FusedAdamEngine:
         hooks = StepHooks(self.comm, callback)  # MULTIGRAD_CHECK_EVERY / MULTIGRAD_METRICS
         err_every = int(os.environ.get("MULTIGRAD_ERR_CHECK_EVERY", "100") or 0)
         with driver_guard(self.comm):
+            comm_bytes = self.comm_bytes_per_step()
             for i in range(start, int(nsteps)):
                 self.step()
                 if hooks.active:
-                    hooks(i, self.loss, self, self.params)
+                    hooks(i, self.loss, self, self.params, comm_bytes=comm_bytes)
                 if err_every and (self.oneshot is not None or self.twoshot is not None) and \
                         (i + 1) % err_every == 0:
                     self.check(collective=True)

@@ -152,6 +152,7 @@ class GraphAdamEngine:
 
     # ------------------------------------------------------------------ the step
     def _sumstats_allreduce(self, S: torch.Tensor) -> torch.Tensor:
+        self._nS = S.numel()
         if self.size == 1:
             return S
         S = S.contiguous()
@@ -338,8 +339,14 @@ class GraphAdamEngine:
                    legacy_bounds_jacobian)
         hooks = StepHooks(self.comm, callback)
         with driver_guard(self.comm):
+            W = self.comm.size
+
+            def comm_bytes():  # sumstat exchange + dense-gradient exchange, bytes sent
+                nS = getattr(self, "_nS", 0)
+                return 0 if W == 1 else int(4 * (W - 1) * (nS + 2 * (self.P // W)))
+
             for i in range(int(nsteps)):
                 self.step()
                 if hooks.active:
-                    hooks(i, self.loss, self, self.params)
+                    hooks(i, self.loss, self, self.params, comm_bytes=comm_bytes)
             return self.trajectory()

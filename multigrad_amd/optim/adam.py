@@ -230,7 +230,9 @@ def run_adam(logloss_and_grad_fn: Callable, params, data, nsteps: int = 100,
             opt.update(torch.as_tensor(grad), traj_row=None if row is None else row.reshape(-1))
             hist.record(step, opt.params())
             if hooks.active:
-                hooks(step, loss, opt, opt.params)
+                g = torch.as_tensor(grad)
+                hooks(step, loss, opt, opt.params,
+                      grad_norm=lambda: float(torch.linalg.vector_norm(g.double())))
             if checkpoint_path and checkpoint_every and (step + 1) % checkpoint_every == 0:
                 ckpt.save_optimizer_state(checkpoint_path, {
                     "adam": opt.state_dict(), "randkey": None if key is None else key.value,

@@ -8,7 +8,10 @@ Environment knobs (read when a driver starts):
     :class:`~multigrad_amd.utils.debug.CollectiveMismatch` unless every rank holds the
     same bits (the SPMD optimizers keep them identical by construction; this verifies it).
 ``MULTIGRAD_METRICS=path``
-    append one JSON record per step (step, loss, step time) to ``path`` on rank 0.
+    append one JSON record per step to ``path`` on rank 0: step, loss, step time, and
+    what the driver knows besides -- the gradient norm (generic Adam), the bytes this
+    rank sent through collectives in the step and the resulting effective rate
+    (``comm_bytes``, ``comm_GBps``: the engines).
 ``MULTIGRAD_METRICS_EVERY=k``
     log every k-th step only (default 1).
 
@@ -50,11 +53,15 @@ class StepHooks:
     def active(self) -> bool:
         return bool(self.callback or self.metrics or self.check_every)
 
-    def __call__(self, step: int, loss, state=None, params_fn: Optional[Callable] = None) -> None:
+    def __call__(self, step: int, loss, state=None, params_fn: Optional[Callable] = None,
+                 **extra) -> None:
+        """``extra``: additional metrics fields (values or zero-argument callables, which
+        are only evaluated when a metrics record is written)."""
         if self.callback is not None:
             self.callback(step, loss, state)
         if self.metrics is not None:
-            self.metrics(step, loss, state)
+            self.metrics(step, loss, state,
+                         **{k: (v() if callable(v) else v) for k, v in extra.items()})
         if self.check_every and params_fn is not None and (step + 1) % self.check_every == 0:
             from .debug import check_consistent
             check_consistent(params_fn(), self.comm, f"{self.what} after step {step}")

@@ -36,10 +36,13 @@ class MetricsLogger:
     def step(self, step: int, loss=None, **extra) -> None:
         if step % self.every:
             return
+        lossf = None if loss is None else float(torch.as_tensor(loss).reshape(-1)[0])  # syncs
         now = time.perf_counter()
         dt, self._t = now - self._t, now
-        self.log(step=step, loss=None if loss is None else float(torch.as_tensor(loss).reshape(-1)[0]),
-                 step_time_s=dt / self.every, **extra)
+        per = dt / self.every
+        if extra.get("comm_bytes") and per > 0:
+            extra["comm_GBps"] = float(f"{float(extra['comm_bytes']) / per / 1e9:.4g}")
+        self.log(step=step, loss=lossf, step_time_s=per, **extra)
 
 
 def _jsonable(v):
@@ -57,7 +60,7 @@ def metrics_callback(path: Optional[str] = None, comm=None, every: int = 1):
         return None
     logger = MetricsLogger(path, comm=comm, every=every)
 
-    def cb(step, loss, state=None):
-        logger.step(step, loss)
+    def cb(step, loss, state=None, **extra):
+        logger.step(step, loss, **extra)
 
     return cb

@@ -70,6 +70,31 @@ def test_metrics_env_installs_logger_in_every_driver(tmp_path, monkeypatch):
     assert len(recs) == n_generic + 2
     assert all("step" in r and "loss" in r and "step_time_s" in r for r in recs)
     assert [r["step"] for r in recs[:3]] == [0, 1, 2]
+    assert all(r["grad_norm"] > 0 for r in recs[:3])          # generic Adam
+    assert all(r.get("comm_bytes") == 0 for r in recs[-2:])    # engine, one rank
+
+
+def _engine_metrics(rank, size, path):
+    os.environ["MULTIGRAD_METRICS"] = path
+    from multigrad_amd.models.population import PopulationSMFModel, make_population_data
+    comm = mg.get_world_comm()
+    data = make_population_data(400, 4000, seed=3, comm=comm, device=torch.device("cpu"))
+    pm = PopulationSMFModel(aux_data=data, comm=comm)
+    pm.set_target_from_truth()
+    pm.run_adam(data["guess"], nsteps=3, learning_rate=1e-3)
+    return rank
+
+
+def test_engine_metrics_report_collective_bytes(tmp_path):
+    """Two ranks, hashed placement (dense gradient): every record carries the bytes the
+    rank sent through collectives in the step and the effective rate."""
+    path = str(tmp_path / "m.jsonl")
+    run_distributed(_engine_metrics, 2, path)
+    recs = [json.loads(line) for line in open(path).read().splitlines()]
+    assert len(recs) == 3
+    # 10 sumstats + 2 (W-1)/W of the padded 400-vector, fp32
+    assert all(r["comm_bytes"] >= 4 * (10 + 400) for r in recs)
+    assert all(r["comm_GBps"] > 0 for r in recs)
 
 
 # ------------------------------------------------------------------ MULTIGRAD_FINGERPRINT
