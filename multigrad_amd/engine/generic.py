@@ -66,6 +66,8 @@ class GraphAdamEngine:
         self.fallback_reason = None
         self.oneshot = None
         self.twoshot = None
+        self.ar = None
+        self.mode = "adam"   # "sgd": fixed-rate gradient descent (run_simple_grad_descent)
 
     # ------------------------------------------------------------------ setup
     def setup(self, guess, nsteps: int, param_bounds=None, learning_rate: float = 0.01,
@@ -83,11 +85,17 @@ class GraphAdamEngine:
         self.legacy = bool(legacy_bounds_jacobian)
         bounds = Bounds.from_spec(param_bounds, P, device=dev)
         cuda = dev.type == "cuda"
+        sgd = self.mode == "sgd"
+        self.ar = None
         if cuda and W > 1:
-            from ..parallel.xgmi import connect_twoshot, get_oneshot, twoshot_enabled
+            from ..parallel.xgmi import (connect_twoshot, get_oneshot, get_twoshot_allreduce,
+                                         twoshot_enabled)
             q = 4 * W
             P_pad = -(-P // q) * q
-            self.twoshot = connect_twoshot(self.comm, P_pad) if twoshot_enabled() else None
+            if sgd:  # the summed gradient itself is needed: a capturable all-reduce
+                self.ar = get_twoshot_allreduce(self.comm, P)
+            else:
+                self.twoshot = connect_twoshot(self.comm, P_pad) if twoshot_enabled() else None
             self.oneshot = get_oneshot(self.comm)
         else:
             P_pad = P
@@ -137,10 +145,14 @@ class GraphAdamEngine:
         else:
             self.traj_loc = None
             self.history = History(history, nsteps, self.p[:P].clone())
+        if sgd:  # losses and the parameters they were evaluated at, indexed on the device
+            self.loss_hist = torch.zeros(self.nsteps, **f32)
+            self.param_hist = torch.zeros((self.nsteps, P), **f32)
         self.graph = None
         self.tuning = None
         self._times = {}
-        capturable = cuda and (W == 1 or (self.twoshot is not None and self.oneshot is not None))
+        exch = self.ar if sgd else self.twoshot
+        capturable = cuda and (W == 1 or (exch is not None and self.oneshot is not None))
         if self.graph_req is True and not capturable:
             raise RuntimeError("this step is not capturable (RCCL collectives in it)")
         self.use_graph = capturable and self.graph_req is not False
@@ -180,6 +192,21 @@ class GraphAdamEngine:
         self.loss.copy_(loss.detach().reshape(1).to(torch.float32))
         g = torch.zeros(self.shape, device=self.device) if g is None else g
         g = g.reshape(-1).to(torch.float32)
+        if self.mode == "sgd":
+            # record (loss, parameters at evaluation) at the device step, then p -= lr g;
+            # the step counter advances on the device, so eager steps and replays agree
+            idx = self.step_dev[:1].long()
+            self.loss_hist.index_copy_(0, idx, self.loss)
+            self.param_hist.index_copy_(0, idx, self.p[:P].view(1, P))
+            if self.size > 1:
+                g = g.contiguous()
+                if self.ar is not None:
+                    self.ar.all_reduce_(g)
+                else:
+                    self.comm.all_reduce(g)
+            self.p[:P].add_(g, alpha=-self.lr)
+            self.step_dev[:1].add_(1)
+            return
         hb = self.history.buf.reshape(-1) if self.history.mode == "full" else None
         if self.twoshot is not None:
             self.gbuf[:P].copy_(g)
@@ -273,7 +300,8 @@ class GraphAdamEngine:
 
     def step(self):
         assert self.ready, "call setup() first"
-        if self.step_host >= self.nsteps and (self.history.mode == "full" or self.traj_loc is not None):
+        if self.step_host >= self.nsteps and (self.history.mode == "full" or self.traj_loc is not None
+                                              or self.mode == "sgd"):
             raise RuntimeError("more steps than the trajectory buffer was sized for")
         if self.use_graph and self.graph_req is None and self.tuning is None and \
                 self.nsteps > 2 * self._TUNE:
@@ -302,7 +330,7 @@ class GraphAdamEngine:
     # ------------------------------------------------------------------ results
     def check(self, where: str = "", collective: bool = False) -> None:
         comm = self.comm if collective else None
-        for ctx in (self.twoshot, self.oneshot):
+        for ctx in (self.twoshot, self.ar, self.oneshot):
             if ctx is not None:
                 ctx.check(where or f"generic engine step {self.step_host}", comm=comm)
 
@@ -328,6 +356,27 @@ class GraphAdamEngine:
         t = self.history.result()[:, :self.P] if self.history.mode == "full" else self.history.result()
         return t.reshape((t.shape[0],) + self.shape)
 
+    def run_simple_grad_descent(self, guess, nsteps: int = 100, learning_rate: float = 0.01,
+                                callback=None):
+        """Fixed-rate gradient descent with the reference's result contract
+        (``GradDescentResult``: ``loss[i]`` and the ``params[i]`` it was evaluated at,
+        multigrad/util.py:100-134), one captured step replayed per iteration."""
+        from ..utils.hooks import StepHooks, driver_guard
+        from ..utils.util import GradDescentResult
+        self.mode = "sgd"
+        self.setup(guess, nsteps, learning_rate=learning_rate, history="last")
+        hooks = StepHooks(self.comm, callback)
+        with driver_guard(self.comm):
+            for i in range(int(nsteps)):
+                self.step()
+                if hooks.active:
+                    hooks(i, self.loss, None, self.params)
+        self.check("simple_grad_descent", collective=True)
+        n = self.step_host
+        return GradDescentResult(loss=self.loss_hist[:n].clone(),
+                                 params=self.param_hist[:n].reshape((n,) + self.shape).clone(),
+                                 aux=[None] * n)
+
     def run_adam(self, guess, nsteps: int = 100, param_bounds=None, learning_rate: float = 0.01,
                  b1: float = 0.9, b2: float = 0.999, eps: float = 1e-8, history="full",
                  legacy_bounds_jacobian: bool = False, callback=None, **unused):
@@ -335,6 +384,7 @@ class GraphAdamEngine:
         if unused:
             raise TypeError(f"unsupported run_adam options for the graph engine: {sorted(unused)}")
         from ..utils.hooks import StepHooks, driver_guard
+        self.mode = "adam"
         self.setup(guess, nsteps, param_bounds, learning_rate, b1, b2, eps, history,
                    legacy_bounds_jacobian)
         hooks = StepHooks(self.comm, callback)

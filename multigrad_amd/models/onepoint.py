@@ -56,6 +56,15 @@ class _OptimizerFrontEnds:
         which ``loss[i]`` was evaluated.
         """
         has_aux = bool(getattr(self, "loss_func_has_aux", False))
+        x0 = as_param_tensor(guess, device=self.param_device())
+        if (x0.is_cuda and x0.dtype == torch.float32 and not has_aux
+                and not getattr(self, "sumstats_func_has_aux", False)
+                and getattr(self, "fused_engine", None) is None
+                and os.environ.get("MULTIGRAD_GENERIC_ENGINE", "1") != "0"):
+            # one captured step replayed per iteration (engine/generic.py)
+            from ..engine.generic import GraphAdamEngine
+            return GraphAdamEngine(self, comm=self._opt_comm()).run_simple_grad_descent(
+                x0, nsteps=nsteps, learning_rate=learning_rate)
         return util.simple_grad_descent(
             None, guess=as_param_tensor(guess, device=self.param_device()), nsteps=nsteps,
             learning_rate=learning_rate,
