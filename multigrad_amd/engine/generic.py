@@ -85,7 +85,7 @@ class GraphAdamEngine:
         self.legacy = bool(legacy_bounds_jacobian)
         bounds = Bounds.from_spec(param_bounds, P, device=dev)
         cuda = dev.type == "cuda"
-        sgd = self.mode == "sgd"
+        sgd = self.mode in ("sgd", "eval")   # modes that need the summed gradient itself
         self.ar = None
         if cuda and W > 1:
             from ..parallel.xgmi import (connect_twoshot, get_oneshot, get_twoshot_allreduce,
@@ -145,9 +145,11 @@ class GraphAdamEngine:
         else:
             self.traj_loc = None
             self.history = History(history, nsteps, self.p[:P].clone())
-        if sgd:  # losses and the parameters they were evaluated at, indexed on the device
+        if self.mode == "sgd":  # losses and the parameters they were evaluated at
             self.loss_hist = torch.zeros(self.nsteps, **f32)
             self.param_hist = torch.zeros((self.nsteps, P), **f32)
+        if self.mode == "eval":  # loss and summed gradient, packed for one host copy
+            self.lg = torch.zeros(1 + P, **f32)
         self.graph = None
         self.tuning = None
         self._times = {}
@@ -192,6 +194,16 @@ class GraphAdamEngine:
         self.loss.copy_(loss.detach().reshape(1).to(torch.float32))
         g = torch.zeros(self.shape, device=self.device) if g is None else g
         g = g.reshape(-1).to(torch.float32)
+        if self.mode == "eval":
+            if self.size > 1:
+                g = g.contiguous()
+                if self.ar is not None:
+                    self.ar.all_reduce_(g)
+                else:
+                    self.comm.all_reduce(g)
+            self.lg[:1].copy_(self.loss)
+            self.lg[1:].copy_(g)
+            return
         if self.mode == "sgd":
             # record (loss, parameters at evaluation) at the device step, then p -= lr g;
             # the step counter advances on the device, so eager steps and replays agree
@@ -355,6 +367,38 @@ class GraphAdamEngine:
             return full.reshape((rows,) + self.shape)
         t = self.history.result()[:, :self.P] if self.history.mode == "full" else self.history.result()
         return t.reshape((t.shape[0],) + self.shape)
+
+    def evaluator(self, x0):
+        """``f(x) -> (loss, grad)`` replaying one captured evaluation of the distributed
+        chain rule (autograd forward, sumstat all-reduce, cotangent, VJP, gradient sum):
+        the objective of the root-driven scipy L-BFGS-B (optim/bfgs.py), which calls it
+        once per function evaluation.  Falls back to eager launches when the step cannot
+        be captured; collective on several ranks (every rank evaluates every point)."""
+        self.mode = "eval"
+        self.setup(x0, nsteps=1, history="last")
+        P, shape = self.P, self.shape
+        if self.use_graph and self.graph_req is not False:
+            try:
+                self.graph = self._capture()
+            except Exception as exc:  # noqa: BLE001  (host sync in user code, ...)
+                if self.graph_req is True or self.size > 1:
+                    raise
+                torch.cuda.synchronize()
+                self.use_graph = False
+                self.fallback_reason = f"capture failed: {type(exc).__name__}: {exc}"
+
+        def f(x, **kw):
+            if kw:
+                raise TypeError(f"the captured evaluator takes no keywords: {sorted(kw)}")
+            self.p[:P].copy_(torch.as_tensor(x).reshape(-1))
+            if self.use_graph:
+                self.graph.replay()
+            else:
+                self._body(None)
+            out = self.lg.cpu()  # loss and gradient in ONE device->host copy
+            return out[0], out[1:].reshape(shape)
+
+        return f
 
     def run_simple_grad_descent(self, guess, nsteps: int = 100, learning_rate: float = 0.01,
                                 callback=None):

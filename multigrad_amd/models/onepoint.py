@@ -134,7 +134,16 @@ class _OptimizerFrontEnds:
         if method == "auto":
             method = "device" if x0.numel() > 100_000 else "scipy"
         if method == "scipy":
-            return _bfgs.run_bfgs(self.calc_loss_and_grad_from_params, x0, maxsteps=maxsteps,
+            fn = self.calc_loss_and_grad_from_params
+            if (randkey is None and x0.is_cuda and x0.dtype == torch.float32
+                    and not getattr(self, "loss_func_has_aux", False)
+                    and not getattr(self, "sumstats_func_has_aux", False)
+                    and getattr(self, "fused_engine", None) is None
+                    and os.environ.get("MULTIGRAD_GENERIC_ENGINE", "1") != "0"):
+                # each scipy evaluation replays one captured evaluation (engine/generic.py)
+                from ..engine.generic import GraphAdamEngine
+                fn = GraphAdamEngine(self, comm=comm).evaluator(x0)
+            return _bfgs.run_bfgs(fn, x0, maxsteps=maxsteps,
                                   param_bounds=param_bounds, randkey=randkey, comm=comm,
                                   device=self.param_device(), **kw)
         from ..optim import lbfgs as _lbfgs
