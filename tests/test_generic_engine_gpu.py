@@ -141,3 +141,25 @@ def test_captured_evaluator_drives_scipy_bfgs(monkeypatch):
     assert res.nit == ref.nit and res.nfev == ref.nfev
     np.testing.assert_allclose(res.x, ref.x, rtol=1e-6, atol=1e-7)
     np.testing.assert_allclose(res.x, [-2.0, -0.5], atol=2e-3)
+
+
+def _bfgs_two(rank, size, engine):
+    os.environ["MULTIGRAD_GENERIC_ENGINE"] = "1" if engine else "0"
+    import multigrad_amd as mg
+    from multigrad_amd.models.smf import DocsSMFModel, make_docs_data
+    comm = mg.get_world_comm()
+    data = make_docs_data(comm=comm)
+    model = DocsSMFModel(aux_data=data, comm=comm)
+    res = model.run_bfgs(torch.tensor([-3.5, 0.2]), method="scipy")
+    return np.asarray(res.x), int(res.nit), float(res.fun)
+
+
+def test_captured_evaluator_two_ranks():
+    """Root-driven scipy L-BFGS-B on two ranks sharing one GPU: the workers replay the
+    captured evaluation (one-shot sumstats, two-shot gradient sum inside the graph) in the
+    root's command loop; same result on both ranks, matching the eager path."""
+    eng = run_distributed(_bfgs_two, 2, True, timeout=600)
+    ref = run_distributed(_bfgs_two, 2, False, timeout=600)
+    np.testing.assert_array_equal(eng[0][0], eng[1][0])
+    np.testing.assert_allclose(eng[0][0], ref[0][0], rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(eng[0][0], [-2.0, -0.5], atol=2e-3)
