@@ -270,3 +270,38 @@ def test_ingraph_descent_multirank_captured_matches_rccl():
     for k in range(20):
         np.testing.assert_allclose(out[0][0][k], p, rtol=1e-4, atol=1e-5)
         p = p - 0.3 * (p - mean)
+
+
+@pytest.mark.parametrize("size", [3, 4, 8])
+def test_twoshot_protocol_more_ranks(size):
+    """The flag protocol, the rank-order sum and graph replay with 3, 4 and 8 processes
+    sharing one GPU (the driver's 8-GPU node runs 8): every rank ends with the same bits,
+    equal to the fp32 sum in rank order."""
+    numel = 4 * size * 257
+    out = run_distributed(_protocol, size, numel, 3, timeout=600)
+    grads = [o[0] for o in out]
+    for rep in range(3):
+        want = grads[0][rep].astype(np.float32)
+        for r in range(1, size):
+            want = (want + grads[r][rep]).astype(np.float32)
+        for o in out:
+            np.testing.assert_array_equal(o[1][rep], want)
+    for o in out:
+        assert o[3]
+        for x in o[2]:
+            np.testing.assert_array_equal(x, np.full(numel, size * (size + 1) / 2, dtype=np.float32))
+
+
+@pytest.mark.parametrize("size", [4, 8])
+def test_engine_hashed_twoshot_more_ranks(size):
+    """The hashed engine step with 4 and 8 ranks on one GPU: the two-shot trajectory is the
+    same on every rank and matches the RCCL/gloo path.  From 3 ranks on, the two paths add
+    the W gradients in different orders (two-shot: fixed rank order; gloo: its ring/tree),
+    so they agree to fp32 rounding rather than bitwise."""
+    ref = run_distributed(_engine_hashed, size, False, False, 2, "auto", None, "on", timeout=900)
+    res = run_distributed(_engine_hashed, size, True, False, 2, "auto", None, "on", timeout=900)
+    assert all(r[1] for r in res) and not any(r[1] for r in ref)
+    for r in range(size):
+        np.testing.assert_array_equal(res[r][0], res[0][0])
+        np.testing.assert_array_equal(ref[r][0], ref[0][0])
+    np.testing.assert_allclose(res[0][0], ref[0][0], rtol=1e-6, atol=1e-7)
