@@ -357,7 +357,8 @@ class FusedAdamEngine:
             cands = [{"ts_side": False}, {"ts_side": True}]   # hashed: where the exchange runs
         elif self._graph_auto and self.capturable and (self.size == 1 or self.owner):
             cands = [{"use_graph": False}, {"use_graph": True}]  # eager launches vs replay
-        if cands and dev.type == "cuda" and _env_flag("MULTIGRAD_AUTOTUNE", True):
+        if cands and dev.type == "cuda" and _env_flag("MULTIGRAD_AUTOTUNE", True) and \
+                not getattr(self, "_skip_autotune", False):
             self._autotune(cands, min_window_s=1e-3 * float(
                 os.environ.get("MULTIGRAD_AUTOTUNE_WINDOW_MS", "30")))
         return self
@@ -877,7 +878,11 @@ class FusedAdamEngine:
     def lbfgs_objective(self, guess):
         """Objective over this rank's optimizer-owned parameters for
         :func:`multigrad_amd.optim.lbfgs.lbfgs_minimize` (sharded under ZeRO)."""
-        self.setup(guess, nsteps=1, history="last")
+        self._skip_autotune = True  # the objective never runs optimizer steps
+        try:
+            self.setup(guess, nsteps=1, history="last")
+        finally:
+            self._skip_autotune = False
         return _EngineObjective(self)
 
     # ------------------------------------------------------------------ checkpoints
