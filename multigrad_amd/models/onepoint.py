@@ -49,6 +49,16 @@ class _OptimizerFrontEnds:
     def param_device(self) -> torch.device:
         raise NotImplementedError
 
+    def _generic_engine_ok(self, x0) -> bool:
+        """Whether this model's GD / scipy-BFGS evaluations can go through the captured
+        generic engine: a single torch OnePointModel (not a group) on a GPU, fp32, no aux
+        outputs, without the fused-engine protocol, not disabled."""
+        return (isinstance(self, OnePointModel) and x0.is_cuda and x0.dtype == torch.float32
+                and not getattr(self, "loss_func_has_aux", False)
+                and not getattr(self, "sumstats_func_has_aux", False)
+                and getattr(self, "fused_engine", None) is None
+                and os.environ.get("MULTIGRAD_GENERIC_ENGINE", "1") != "0")
+
     def run_simple_grad_descent(self, guess, nsteps: int = 100, learning_rate: float = 0.01):
         """Fixed-learning-rate gradient descent.
 
@@ -57,10 +67,7 @@ class _OptimizerFrontEnds:
         """
         has_aux = bool(getattr(self, "loss_func_has_aux", False))
         x0 = as_param_tensor(guess, device=self.param_device())
-        if (x0.is_cuda and x0.dtype == torch.float32 and not has_aux
-                and not getattr(self, "sumstats_func_has_aux", False)
-                and getattr(self, "fused_engine", None) is None
-                and os.environ.get("MULTIGRAD_GENERIC_ENGINE", "1") != "0"):
+        if self._generic_engine_ok(x0):
             # one captured step replayed per iteration (engine/generic.py)
             from ..engine.generic import GraphAdamEngine
             return GraphAdamEngine(self, comm=self._opt_comm()).run_simple_grad_descent(
@@ -105,7 +112,7 @@ class _OptimizerFrontEnds:
         graph_kw = {k: kw[k] for k in kw if k in ("history", "legacy_bounds_jacobian", "b1",
                                                    "b2", "eps", "callback")}
         if fused is None and use_engine and randkey is None and not const_randkey and \
-                len(graph_kw) == len(kw) and guess.is_cuda and \
+                isinstance(self, OnePointModel) and len(graph_kw) == len(kw) and guess.is_cuda and \
                 not getattr(self, "sumstats_func_has_aux", False) and \
                 os.environ.get("MULTIGRAD_GENERIC_ENGINE", "1") != "0":
             from ..engine.generic import GraphAdamEngine
@@ -135,11 +142,7 @@ class _OptimizerFrontEnds:
             method = "device" if x0.numel() > 100_000 else "scipy"
         if method == "scipy":
             fn = self.calc_loss_and_grad_from_params
-            if (randkey is None and x0.is_cuda and x0.dtype == torch.float32
-                    and not getattr(self, "loss_func_has_aux", False)
-                    and not getattr(self, "sumstats_func_has_aux", False)
-                    and getattr(self, "fused_engine", None) is None
-                    and os.environ.get("MULTIGRAD_GENERIC_ENGINE", "1") != "0"):
+            if randkey is None and self._generic_engine_ok(x0):
                 # each scipy evaluation replays one captured evaluation (engine/generic.py)
                 from ..engine.generic import GraphAdamEngine
                 fn = GraphAdamEngine(self, comm=comm).evaluator(x0)

@@ -85,3 +85,9 @@ def test_onepoint_group_on_rccl_subcommunicators(monkeypatch):
     assert grad.is_cuda and loss.is_cuda
     res = grp.run_bfgs(p, maxsteps=30)
     assert res.success or res.nit > 0
+    # the group's GD / Adam front-ends keep the eager loop (the captured engine takes
+    # single models only)
+    gd = grp.run_simple_grad_descent(p, nsteps=3, learning_rate=1e-3)
+    assert gd.params.shape == (3, 2) and torch.isfinite(gd.loss).all()
+    traj = grp.run_adam(p, nsteps=3, learning_rate=1e-3)
+    assert tuple(traj.shape) == (4, 2)
