@@ -162,8 +162,8 @@ class PopulationShard:
             pop = torch.as_tensor(pop).reshape(-1)
             if pop.device.type == "cuda":
                 # device radix sort + histogram; only the J counts come back to the host
-                spop, order = torch.sort(pop.to(torch.int32), stable=True)
-                counts = torch.bincount(spop, minlength=self.npop).cpu().to(torch.int64)
+                spop, order, counts = stable_population_sort(pop.to(torch.int32), self.npop)
+                counts = counts.cpu().to(torch.int64)
                 xs = x.reshape(-1).to(pop.device)[order].to(device=device, dtype=torch.float32)
                 self.pop = spop.to(device).contiguous()
                 del order
@@ -367,6 +367,41 @@ def _sort_by_population(pop_cpu: torch.Tensor, npop: int):
         order = torch.argsort(pop_cpu.long(), stable=True)
         counts = torch.bincount(pop_cpu.long(), minlength=npop)
         return order, counts
+
+
+_SORT_CHUNK = 1 << 30  # torch.sort refuses more than INT_MAX elements
+
+
+def stable_population_sort(pop: torch.Tensor, npop: int, chunk: Optional[int] = None):
+    """``(sorted_pop, order, counts)`` of a stable sort of the int32 population ids, on
+    the ids' device.  Up to ``chunk`` elements this is one radix sort.  Longer shards (a
+    288 GB GPU holds several 1e9 halos) are sorted in chunks and placed by a stable
+    counting sort across them: a halo of population p that is the r-th of p in chunk c
+    goes to ``start[p] + (p's count in chunks < c) + r`` -- the same order one global
+    stable sort would give."""
+    chunk = _SORT_CHUNK if chunk is None else int(chunk)
+    n = pop.numel()
+    if n <= chunk:
+        spop, order = torch.sort(pop, stable=True)
+        return spop, order, torch.bincount(spop, minlength=npop)
+    dev = pop.device
+    counts = torch.zeros(npop, dtype=torch.int64, device=dev)
+    for c0 in range(0, n, chunk):
+        counts += torch.bincount(pop[c0:c0 + chunk], minlength=npop)
+    placed = torch.cumsum(counts, 0) - counts      # start of p, then + p's halos so far
+    order = torch.empty(n, dtype=torch.int64, device=dev)
+    for c0 in range(0, n, chunk):
+        sp, o = torch.sort(pop[c0:c0 + chunk], stable=True)
+        cc = torch.bincount(sp, minlength=npop)
+        first = torch.cumsum(cc, 0) - cc              # first position of p in this chunk
+        sp64 = sp.long()
+        pos = placed[sp64] + (torch.arange(sp.numel(), device=dev) - first[sp64])
+        order[pos] = o + c0
+        placed += cc
+        del sp, o, cc, first, sp64, pos
+    spop = torch.repeat_interleave(torch.arange(npop, dtype=torch.int32, device=dev), counts,
+                                   output_size=n)
+    return spop, order, counts
 
 
 def _build_tiles(counts, breaks, tile_halos, tile_pops):

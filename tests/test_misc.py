@@ -122,3 +122,16 @@ def _consistency_body(rank, size):
 def test_debug_aids_detect_divergence():
     res = run_distributed(_consistency_body, 2)
     assert all(r == (True, True) for r in res)
+
+
+def test_stable_population_sort_chunked_matches_one_sort():
+    """Shards beyond torch.sort's INT_MAX limit are sorted in chunks and placed by a stable
+    counting sort: the same order, ids and counts as one stable sort."""
+    from multigrad_amd.ops.smf import stable_population_sort
+    g = torch.Generator().manual_seed(0)
+    for n, npop, chunk in [(10000, 37, 1000), (12345, 5000, 999), (5000, 3, 5000), (7, 100, 2)]:
+        pop = torch.randint(0, npop, (n,), generator=g, dtype=torch.int32)
+        spop, order, counts = stable_population_sort(pop, npop, chunk=chunk)
+        ref_s, ref_o = torch.sort(pop, stable=True)
+        assert torch.equal(spop, ref_s) and torch.equal(order, ref_o)
+        assert torch.equal(counts, torch.bincount(pop, minlength=npop))
