@@ -311,6 +311,12 @@ class FusedAdamEngine:
         self._ag: List = [None] * self.C
         self.comm_stream = None
         self.ts_side = False
+        # hashed placement with the two-shot context up: RCCL reduce-scatter / all-gather
+        # stays available as an autotune candidate (on the same buffers and shard layout)
+        self.rccl_exchange = False
+        xmode = os.environ.get("MULTIGRAD_HASHED_EXCHANGE", "auto").strip().lower()
+        if self.twoshot is not None and xmode == "rccl":
+            self.rccl_exchange = True
         side_mode = _side_stream_mode()
         if self.twoshot is not None and self.C > 1 and side_mode != "off":
             # overlapped schedule: the two-shot exchange of chunk c runs on a side stream as
@@ -353,8 +359,15 @@ class FusedAdamEngine:
         self._tuning = False
         self.ready = True
         cands = []
-        if self.comm_stream is not None and side_mode == "auto" and not self.use_graph:
-            cands = [{"ts_side": False}, {"ts_side": True}]   # hashed: where the exchange runs
+        if self.comm_stream is not None and side_mode == "auto" and not self.use_graph and \
+                xmode != "rccl":
+            # hashed: where the exchange runs -- two-shot on the compute stream, on the side
+            # stream, or RCCL's reduce-scatter / all-gather (measured, not assumed;
+            # MULTIGRAD_HASHED_EXCHANGE=twoshot|rccl pins it)
+            cands = [{"ts_side": False, "rccl_exchange": False},
+                     {"ts_side": True, "rccl_exchange": False}]
+            if xmode != "twoshot":
+                cands.append({"ts_side": False, "rccl_exchange": True})
         elif self._graph_auto and self.capturable and (self.size == 1 or self.owner):
             cands = [{"use_graph": False}, {"use_graph": True}]  # eager launches vs replay
         if cands and dev.type == "cuda" and _env_flag("MULTIGRAD_AUTOTUNE", True) and \
@@ -655,7 +668,7 @@ class FusedAdamEngine:
                            self.b1, self.b2, self.eps, self.bounds_loc, self.legacy,
                            traj_base=tb, traj_stride=(b - a) if tb is not None else 0,
                            host_step=self._hstep())
-        elif self.zero and self.twoshot is not None:
+        elif self.zero and self.twoshot is not None and not self.rccl_exchange:
             for c in range(self.C):
                 with self._ph("vjp"):
                     md.engine_vjp_into(self.theta, self.h, self.grad, chunk=c)
@@ -848,6 +861,9 @@ class FusedAdamEngine:
             return "none (1 rank)"
         if self.owner:
             return "none: owner-local gradients, sumstat all-reduce only"
+        if self.zero and self.twoshot is not None and self.rccl_exchange:
+            return ("RCCL reduce-scatter + all-gather (ZeRO-1), measured faster than the "
+                    "two-shot kernel at setup")
         if self.zero and self.twoshot is not None:
             sched = (f", {self.C} chunks on a side stream overlapping compute" if self.ts_side
                      else f", {self.C} chunk(s) on the compute stream")

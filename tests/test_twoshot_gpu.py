@@ -183,6 +183,23 @@ def test_engine_hashed_twoshot_matches_rccl_path(bounded, chunks, layout, side):
     np.testing.assert_array_equal(res[0][0], ref[0][0])  # bitwise: same sums, same Adam bits
 
 
+def _engine_hashed_rccl(rank, size, bounded):
+    os.environ["MULTIGRAD_HASHED_EXCHANGE"] = "rccl"
+    return _engine_hashed(rank, size, True, bounded, 2, "auto", None, "off")
+
+
+@pytest.mark.parametrize("bounded", [False, True])
+def test_engine_hashed_rccl_exchange_candidate(bounded):
+    """The RCCL reduce-scatter / all-gather candidate of the hashed autotune, run on the
+    two-shot context's buffers and shard layout (MULTIGRAD_HASHED_EXCHANGE=rccl): the
+    same trajectory as the engine without a two-shot context."""
+    ref = run_distributed(_engine_hashed, 2, False, bounded, 2, "auto", None, "off", timeout=600)
+    res = run_distributed(_engine_hashed_rccl, 2, bounded, timeout=600)
+    assert res[0][1] and "RCCL" in res[0][4], res[0][4]
+    np.testing.assert_array_equal(res[0][0], res[1][0])
+    np.testing.assert_array_equal(res[0][0], ref[0][0])
+
+
 @pytest.mark.parametrize("bounded", [False, True])
 def test_engine_hashed_twoshot_graph_replay_matches_eager(bounded):
     """The whole hashed step (forward, one-shot epilogue, VJP, two-shot exchange) captured
