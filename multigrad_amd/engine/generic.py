@@ -158,6 +158,12 @@ class GraphAdamEngine:
         if self.graph_req is True and not capturable:
             raise RuntimeError("this step is not capturable (RCCL collectives in it)")
         self.use_graph = capturable and self.graph_req is not False
+        if self.use_graph and W > 1 and not self._probe_capture():
+            # a rank's user hooks cannot be captured: every rank runs eagerly (a per-rank
+            # fallback would leave the ranks' collective sequences out of step)
+            if self.graph_req is True:
+                raise RuntimeError(f"the step is not capturable: {self.fallback_reason}")
+            self.use_graph = False
         if not capturable and self.graph_req is None:
             self.fallback_reason = "RCCL / gloo collectives in the step" if W > 1 else \
                 "CPU tensors"
@@ -165,6 +171,43 @@ class GraphAdamEngine:
         return self
 
     # ------------------------------------------------------------------ the step
+    def _hooks_only(self):
+        """The user's part of a step (forward, loss, cotangent, VJP) without collectives."""
+        md, P = self.model, self.P
+        with torch.enable_grad():
+            leaf = self.p[:P].detach().view(self.shape).requires_grad_(True)
+            partial = torch.as_tensor(md.calc_partial_sumstats_from_params(leaf))
+            total = partial.detach().clone().requires_grad_(True)
+            out = md.calc_loss_from_sumstats(total)
+            loss = out[0] if md.loss_func_has_aux else out
+            (cot,) = torch.autograd.grad(loss, total, allow_unused=True)
+            if cot is not None:
+                torch.autograd.grad(partial, leaf, cot, allow_unused=True)
+
+    def _probe_capture(self) -> bool:
+        """Collective: can every rank capture its user hooks?  Each rank captures the
+        collective-free part of a step into a throw-away graph; the verdicts are all-gathered
+        so all ranks take the same path."""
+        ok, reason = True, None
+        try:
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                self._hooks_only()   # lazy initialisation outside the capture
+            torch.cuda.current_stream().wait_stream(s)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self._hooks_only()
+            del g
+        except Exception as exc:  # noqa: BLE001  (host sync / dynamic shapes in user code)
+            torch.cuda.synchronize()
+            ok, reason = False, f"capture failed: {type(exc).__name__}: {exc}"
+        verdicts = self.comm.allgather((ok, reason))
+        bad = [(r, why) for r, (good, why) in enumerate(verdicts) if not good]
+        if bad:
+            self.fallback_reason = f"rank {bad[0][0]}: {bad[0][1]}"
+        return not bad
+
     def _sumstats_allreduce(self, S: torch.Tensor) -> torch.Tensor:
         self._nS = S.numel()
         if self.size == 1:

@@ -163,3 +163,36 @@ def test_captured_evaluator_two_ranks():
     np.testing.assert_array_equal(eng[0][0], eng[1][0])
     np.testing.assert_allclose(eng[0][0], ref[0][0], rtol=1e-5, atol=1e-6)
     np.testing.assert_allclose(eng[0][0], [-2.0, -0.5], atol=2e-3)
+
+
+def _two_ranks_syncing(rank, size, mode):
+    import multigrad_amd as mg
+    from multigrad_amd.engine.generic import GraphAdamEngine
+    from multigrad_amd.models.torch_population import TorchPopulationSMFModel
+
+    class Syncing(TorchPopulationSMFModel):
+        def calc_partial_sumstats_from_params(self, params, randkey=None):
+            if rank == 1 and float(params.sum()) != float(params.sum()):  # rank 1 only
+                raise ValueError
+            return super().calc_partial_sumstats_from_params(params)
+
+    comm = mg.get_world_comm()
+    m, guess = _torch_pop(comm=comm)
+    s = Syncing(aux_data=m.aux_data, comm=comm)
+    eng = GraphAdamEngine(s)
+    if mode == "adam":
+        out = eng.run_adam(guess, nsteps=4, learning_rate=1e-3).cpu().numpy()
+    else:
+        out = eng.run_simple_grad_descent(guess, nsteps=4, learning_rate=3e-3).params.cpu().numpy()
+    return out, eng.use_graph, eng.fallback_reason
+
+
+@pytest.mark.parametrize("mode", ["adam", "sgd"])
+def test_two_ranks_uncapturable_hooks_fall_back_together(mode):
+    """Only rank 1's hooks synchronise with the host: the collective capture probe sends
+    BOTH ranks down the eager path (no rank replays a graph whose collectives the other
+    rank never issues), and the run completes with identical results."""
+    res = run_distributed(_two_ranks_syncing, 2, mode, timeout=600)
+    assert not res[0][1] and not res[1][1]
+    assert "rank 1" in res[0][2] and "rank 1" in res[1][2]
+    np.testing.assert_array_equal(res[0][0], res[1][0])
