@@ -95,9 +95,11 @@ def run_bfgs(loss_and_grad_fn: Callable, params, maxsteps: int = 100, param_boun
                 hooks(nit[0], None if res is None else float(res.fun), None)
             nit[0] += 1
 
-        result = scipy.optimize.minimize(fun, x0=x0, method="L-BFGS-B", jac=True,
-                                         options=dict(maxiter=maxsteps, **(options or {})),
-                                         callback=callback, bounds=param_bounds)
+        from ..utils.tensors import blas_single_thread
+        with blas_single_thread():  # keep the cores for the model evaluations
+            result = scipy.optimize.minimize(fun, x0=x0, method="L-BFGS-B", jac=True,
+                                             options=dict(maxiter=maxsteps, **(options or {})),
+                                             callback=callback, bounds=param_bounds)
         if pbar is not None:
             pbar.close()
         if multi:

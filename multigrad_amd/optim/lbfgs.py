@@ -96,7 +96,7 @@ def _cubic_min(a, fa, da, b, fb, db):
     return b - (b - a) * (db + d2 - d1) / den
 
 
-def lbfgs_minimize(obj, maxiter: int = 100, m: int = 10, ftol: float = 1e7 * _EPS,
+def _lbfgs_minimize_impl(obj, maxiter: int = 100, m: int = 10, ftol: float = 1e7 * _EPS,
                    gtol: float = 1e-5, maxls: int = 20, c1: float = 1e-4, c2: float = 0.9,
                    callback=None) -> scipy.optimize.OptimizeResult:
     """Minimise ``obj`` (see :class:`GenericObjective`) with L-BFGS; SPMD-consistent."""
@@ -314,3 +314,14 @@ def run_lbfgs_device(loss_and_grad_fn: Callable, params, maxsteps: int = 100, pa
     fkw = {} if randkey is None else {"randkey": init_randkey(randkey)}
     obj = GenericObjective(loss_and_grad_fn, x0, comm=comm, bounds=bounds, **fkw)
     return lbfgs_minimize(obj, maxiter=maxsteps, m=history, **kw)
+
+
+def lbfgs_minimize(*args, **kwargs):
+    """See ``_lbfgs_minimize_impl``; runs with the BLAS pools limited to one thread (the host-side
+    compact-form solves are tiny; a spinning BLAS pool would slow the CPU evaluations)."""
+    from ..utils.tensors import blas_single_thread
+    with blas_single_thread():
+        return _lbfgs_minimize_impl(*args, **kwargs)
+
+
+lbfgs_minimize.__doc__ = _lbfgs_minimize_impl.__doc__

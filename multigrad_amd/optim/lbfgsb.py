@@ -147,7 +147,7 @@ class _History:
         return rows, fac
 
 
-def lbfgsb_minimize(obj, lo=None, hi=None, maxiter: int = 100, m: int = 10,
+def _lbfgsb_minimize_impl(obj, lo=None, hi=None, maxiter: int = 100, m: int = 10,
                     factr: float = 1e7, pgtol: float = 1e-5, maxls: int = 20,
                     c1: float = 1e-4, c2: float = 0.9, K: Optional[int] = None,
                     callback=None, gtol: Optional[float] = None,
@@ -533,3 +533,14 @@ def bounds_arrays(param_bounds, n: int):
         if c is not None:
             hi[i] = float(c)
     return lo.astype(np.float32), hi.astype(np.float32)
+
+
+def lbfgsb_minimize(*args, **kwargs):
+    """See ``_lbfgsb_minimize_impl``; runs with the BLAS pools limited to one thread (the host-side
+    compact-form solves are tiny; a spinning BLAS pool would slow the CPU evaluations)."""
+    from ..utils.tensors import blas_single_thread
+    with blas_single_thread():
+        return _lbfgsb_minimize_impl(*args, **kwargs)
+
+
+lbfgsb_minimize.__doc__ = _lbfgsb_minimize_impl.__doc__
