@@ -358,6 +358,12 @@ class FusedAdamEngine:
         self.tuning = None
         self._tuning = False
         self.ready = True
+        if self.size > 1 and dev.type == "cuda":
+            # line the ranks up before the first peer-memory exchange: a kernel waits for
+            # its peers at most MULTIGRAD_ONESHOT_TIMEOUT, and the setup above (data layout,
+            # sorts, first code-object loads) takes different times on different ranks
+            torch.cuda.synchronize()
+            self.comm.barrier()
         cands = []
         if self.comm_stream is not None and side_mode == "auto" and not self.use_graph and \
                 xmode != "rccl":

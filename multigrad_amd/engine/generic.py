@@ -167,6 +167,11 @@ class GraphAdamEngine:
         if not capturable and self.graph_req is None:
             self.fallback_reason = "RCCL / gloo collectives in the step" if W > 1 else \
                 "CPU tensors"
+        if W > 1 and cuda:
+            # the ranks meet here before the first peer-memory exchange (its wait for a
+            # peer is bounded by MULTIGRAD_ONESHOT_TIMEOUT)
+            torch.cuda.synchronize()
+            self.comm.barrier()
         self.ready = True
         return self
 
