@@ -209,7 +209,21 @@ def main(argv=None):
         order = ["hashed", "owner"]
     else:
         order = [args.placement]
-    res = {p: time_placement(p, args, comm, dev, sync) for p in order}
+    res, errors = {}, {}
+    for i, p in enumerate(order):
+        if i == 0:
+            res[p] = time_placement(p, args, comm, dev, sync)
+            continue
+        # the extra placement must not cost the headline line: a failure that every rank
+        # sees (e.g. out of memory) is reported in the record instead of ending the run
+        try:
+            res[p] = time_placement(p, args, comm, dev, sync)
+        except Exception as exc:  # noqa: BLE001
+            errors[p] = f"{type(exc).__name__}: {exc}"[:300]
+            print(f"bench.py: {p} placement failed: {errors[p]}", file=sys.stderr, flush=True)
+            if dev.type == "cuda":
+                torch.cuda.synchronize()
+                torch.cuda.empty_cache()
     head = res[order[0]]
     own = res.get("owner", head if comm.size == 1 else None)
     history = head["history"]
@@ -253,6 +267,8 @@ def main(argv=None):
         "loss_last": head["loss_last"],
         "setup_s": head["setup_s"],
     }
+    if errors:
+        rec["errors"] = errors
     if own is not None and own is not head:
         rec["owner_config"] = {k: own[k] for k in ("parallelism", "optimizer_sharding",
                                                    "grad_collective", "sumstat_allreduce",
