@@ -154,6 +154,9 @@ __device__ __forceinline__ void halo_mass(float x, float2 th, const SmfBins& b,
 #define MG_FWD_MINWAVES 8
 #endif
 constexpr int kFwdUnroll = MG_FWD_UNROLL;
+#ifndef MG_FWD_PIPE
+#define MG_FWD_PIPE 1
+#endif
 
 template <int NB, bool LOGSIG, bool HAS_POP, bool REL>
 __global__ __launch_bounds__(kThreads, MG_FWD_MINWAVES) void smf_fwd_kernel(
@@ -181,6 +184,50 @@ __global__ __launch_bounds__(kThreads, MG_FWD_MINWAVES) void smf_fwd_kernel(
   // are masked with x = -inf), so the ballot counts stay in SGPRs and are complete
   const int lane = threadIdx.x & (kWave - 1);
   const int wbase = __builtin_amdgcn_readfirstlane(threadIdx.x - lane);
+#if MG_FWD_PIPE
+  // Software pipeline over the grid-stride iterations: the halos of iteration k+2 (x and
+  // population id) and the parameter gather of iteration k+1 are in flight while
+  // iteration k is computed, so neither the id load nor the dependent gather is waited for
+  // behind the math.
+  if constexpr (HAS_POP) {
+    const int64_t step = kFwdUnroll * stride;
+    auto load_xp = [&](int64_t w, float (&xs)[kFwdUnroll], int (&ps)[kFwdUnroll]) {
+#pragma unroll
+      for (int u = 0; u < kFwdUnroll; ++u) {
+        const int64_t i = w + lane + u * stride;
+        const bool ok = i < end;
+        xs[u] = ok ? x[i] : -INFINITY;
+        ps[u] = ok ? pop[i] : 0;
+      }
+    };
+    int64_t w0 = begin + (int64_t)blockIdx.x * kThreads + wbase;
+    float xa[kFwdUnroll], xb[kFwdUnroll];
+    int pa[kFwdUnroll], pb[kFwdUnroll];
+    float2 tha[kFwdUnroll];
+    load_xp(w0, xa, pa);
+#pragma unroll
+    for (int u = 0; u < kFwdUnroll; ++u) tha[u] = theta[pa[u]];
+    load_xp(w0 + step, xb, pb);
+    for (; w0 < end; w0 += step) {
+      float2 thb[kFwdUnroll];
+#pragma unroll
+      for (int u = 0; u < kFwdUnroll; ++u) thb[u] = theta[pb[u]];
+      float xc[kFwdUnroll];
+      int pc[kFwdUnroll];
+      load_xp(w0 + 2 * step, xc, pc);
+#pragma unroll
+      for (int u = 0; u < kFwdUnroll; ++u)
+        halo_mass<NB, LOGSIG, REL, kRepl>(xa[u], tha[u], bins, acc, cnt, tb);
+#pragma unroll
+      for (int u = 0; u < kFwdUnroll; ++u) {
+        xa[u] = xb[u];
+        tha[u] = thb[u];
+        xb[u] = xc[u];
+        pb[u] = pc[u];
+      }
+    }
+  } else
+#endif
   for (int64_t w0 = begin + (int64_t)blockIdx.x * kThreads + wbase; w0 < end;
        w0 += kFwdUnroll * stride) {
     // issue every load of this iteration before any math (one dependent round trip)
@@ -321,10 +368,44 @@ __global__ __launch_bounds__(kThreads) void smf_epilogue_kernel(
 // Per-halo VJP contributions in the scaled coordinate w = z*kWScale:
 //   A += sum_e h_e exp2(-w_e^2),   B += sum_e h_e exp2(-w_e^2) w_e
 // (h_e already carries 1/sqrt(2 pi); B is converted back to z units in pop_grad).
+// MG_VJP_EP: edges two at a time in packed fp32 (v_pk_fma / v_pk_mul / v_pk_add on the
+// pair (edge 2i, edge 2i+1), as in the lanes forward's EdgePairs), so w, w^2, h*g and both
+// accumulations cost one issue per pair; v_exp stays per element.
+#ifndef MG_VJP_EP
+#define MG_VJP_EP 1
+#endif
 template <int NB, bool LOGSIG>
 __device__ __forceinline__ void halo_vjp(float x, float2 th, float inv, const float (&h)[NB + 1],
                                          const SmfBins& b, float& A, float& B) {
   const float nmi = -(x + th.x) * inv;
+#if MG_VJP_EP
+  constexpr int NP = (NB + 1) / 2;
+  v2f Ap = (v2f)(0.0f), Bp = (v2f)(0.0f);
+#pragma unroll
+  for (int i = 0; i < NP; ++i) {
+    v2f e2, h2;
+    e2.x = b.edge[2 * i];
+    e2.y = b.edge[2 * i + 1];
+    h2.x = h[2 * i];
+    h2.y = h[2 * i + 1];
+    const v2f w = e2 * inv + nmi;
+    const v2f q = -w * w;
+    v2f g;
+    g.x = fast_exp2(q.x);
+    g.y = fast_exp2(q.y);
+    const v2f t = h2 * g;
+    Ap = Ap + t;
+    Bp = t * w + Bp;
+  }
+  if constexpr ((NB + 1) & 1) {
+    const float w = fmaf(b.edge[NB], inv, nmi);
+    const float t = h[NB] * fast_exp2(-w * w);
+    Ap.x += t;
+    Bp.x = fmaf(t, w, Bp.x);
+  }
+  A += Ap.x + Ap.y;
+  B += Bp.x + Bp.y;
+#else
 #pragma unroll
   for (int e = 0; e <= NB; ++e) {
     const float w = fmaf(b.edge[e], inv, nmi);
@@ -332,6 +413,7 @@ __device__ __forceinline__ void halo_vjp(float x, float2 th, float inv, const fl
     A += t;
     B = fmaf(t, w, B);
   }
+#endif
 }
 
 // inv is the scaled inverse sigma (kWScale / sigma); A, B from halo_vjp.
