@@ -192,10 +192,20 @@ __global__ __launch_bounds__(kTsThreads) void xgmi_twoshot_kernel(TwoShotArgs a)
   const int64_t stride = (int64_t)gridDim.x * kTsThreads;
   for (int64_t i = (int64_t)blockIdx.x * kTsThreads + threadIdx.x; i < n4; i += stride) {
     const int64_t off = a.lo + 4 * i;
-    float4 g = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(a.g.base[0]) + off);
-    for (int q = 1; q < a.size; ++q) {
-      const float4 h = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(a.g.base[q]) + off);
-      g.x += h.x; g.y += h.y; g.z += h.z; g.w += h.w;
+    // every peer's load is issued before the first add (the peer loop is unrolled to the
+    // compile-time rank limit), so the W remote round trips overlap instead of running one
+    // after another; the sum is still taken in rank order
+    float4 hs[kXMaxRanks];
+#pragma unroll
+    for (int q = 0; q < kXMaxRanks; ++q)
+      if (q < a.size)
+        hs[q] = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(a.g.base[q]) + off);
+    float4 g = hs[0];
+#pragma unroll
+    for (int q = 1; q < kXMaxRanks; ++q) {
+      if (q < a.size) {
+        g.x += hs[q].x; g.y += hs[q].y; g.z += hs[q].z; g.w += hs[q].w;
+      }
     }
     float4 p = g;
     if constexpr (MODE >= 1) {
