@@ -178,6 +178,26 @@ def time_placement(placement, args, comm, dev, sync):
     return info
 
 
+def run_placements(order, timed, on_error=None):
+    """Time each placement in ``order`` with ``timed(placement)``.  The first one is the
+    headline and its failure ends the run; a failure of a later (extra) placement that every
+    rank sees (e.g. out of memory) is returned in ``errors`` instead, so it does not cost the
+    headline line."""
+    res, errors = {}, {}
+    for i, p in enumerate(order):
+        if i == 0:
+            res[p] = timed(p)
+            continue
+        try:
+            res[p] = timed(p)
+        except Exception as exc:  # noqa: BLE001
+            errors[p] = f"{type(exc).__name__}: {exc}"[:300]
+            print(f"bench.py: {p} placement failed: {errors[p]}", file=sys.stderr, flush=True)
+            if on_error is not None:
+                on_error()
+    return res, errors
+
+
 def main(argv=None):
     argv = sys.argv[1:] if argv is None else list(argv)
     args = _args(argv)
@@ -209,21 +229,13 @@ def main(argv=None):
         order = ["hashed", "owner"]
     else:
         order = [args.placement]
-    res, errors = {}, {}
-    for i, p in enumerate(order):
-        if i == 0:
-            res[p] = time_placement(p, args, comm, dev, sync)
-            continue
-        # the extra placement must not cost the headline line: a failure that every rank
-        # sees (e.g. out of memory) is reported in the record instead of ending the run
-        try:
-            res[p] = time_placement(p, args, comm, dev, sync)
-        except Exception as exc:  # noqa: BLE001
-            errors[p] = f"{type(exc).__name__}: {exc}"[:300]
-            print(f"bench.py: {p} placement failed: {errors[p]}", file=sys.stderr, flush=True)
-            if dev.type == "cuda":
-                torch.cuda.synchronize()
-                torch.cuda.empty_cache()
+    def release():
+        if dev.type == "cuda":
+            torch.cuda.synchronize()
+            torch.cuda.empty_cache()
+
+    res, errors = run_placements(order, lambda p: time_placement(p, args, comm, dev, sync),
+                                 on_error=release)
     head = res[order[0]]
     own = res.get("owner", head if comm.size == 1 else None)
     history = head["history"]

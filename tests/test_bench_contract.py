@@ -52,3 +52,27 @@ def test_bench_two_ranks_json(placement):
     assert KEYS <= set(rec) and rec["n_gpus"] == 2
     assert rec["config"]["placement"] == placement
     assert rec["config"]["optimizer_sharding"] == ("owner" if placement == "owner" else "zero1")
+
+
+def test_extra_placement_failure_keeps_the_headline():
+    """A failure of the extra (owner) placement is reported in the record's errors; a
+    failure of the headline placement still ends the run."""
+    import bench
+
+    def timed(p):
+        if p == "owner":
+            raise MemoryError("out of device memory")
+        return {"steps_per_s": 1.0}
+
+    released = []
+    res, errors = bench.run_placements(["hashed", "owner"], timed,
+                                       on_error=lambda: released.append(True))
+    assert res == {"hashed": {"steps_per_s": 1.0}}
+    assert errors["owner"].startswith("MemoryError: out of device memory")
+    assert released == [True]
+
+    def broken(p):
+        raise RuntimeError("headline failed")
+
+    with pytest.raises(RuntimeError):
+        bench.run_placements(["hashed", "owner"], broken)
