@@ -12,3 +12,9 @@ def __getattr__(name):
         import multigrad_amd
         return getattr(multigrad_amd, name)
     raise AttributeError(name)
+
+from multigrad_amd.utils.progress import (trange_no_tqdm, make_trange_with_tqdm,  # noqa: E402,F401
+                                          make_module_trange)
+
+trange_with_tqdm = make_trange_with_tqdm(None)
+trange = make_module_trange(None)

@@ -84,6 +84,16 @@ def test_multigrad_alias_package():
     from multigrad.mpi4jax import distribute_data  # noqa: F401
     assert multigrad.OnePointModel is mg.OnePointModel
     assert multigrad.reduce_sum is mg.reduce_sum
+    # the reference's per-module progress helpers (multigrad/adam.py:28-36, bfgs.py:21-29,
+    # multigrad.py:37-45, util.py:39-47)
+    import multigrad.adam as ma
+    import multigrad.bfgs as mb
+    import multigrad.multigrad as mm
+    import multigrad.util as mu
+    for mod, pick in ((ma, "adam_trange"), (mb, "bfgs_trange"), (mm, "trange"), (mu, "trange")):
+        assert list(mod.trange_no_tqdm(3)) == [0, 1, 2]
+        assert callable(mod.trange_with_tqdm)
+        assert len(list(getattr(mod, pick)(4))) == 4
 
 
 def test_metrics_and_profiling(tmp_path):
