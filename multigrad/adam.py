@@ -8,3 +8,11 @@ from multigrad_amd.utils.progress import (trange_no_tqdm, make_trange_with_tqdm,
 
 trange_with_tqdm = make_trange_with_tqdm('Adam Gradient Descent Progress')
 adam_trange = make_module_trange('Adam Gradient Descent Progress')
+
+
+def __getattr__(name):
+    # the reference's import-time MPI globals (COMM, RANK, N_RANKS in every module)
+    if name in ("COMM", "RANK", "N_RANKS"):
+        import multigrad_amd
+        return getattr(multigrad_amd, name)
+    raise AttributeError(name)

@@ -94,6 +94,7 @@ def test_multigrad_alias_package():
         assert list(mod.trange_no_tqdm(3)) == [0, 1, 2]
         assert callable(mod.trange_with_tqdm)
         assert len(list(getattr(mod, pick)(4))) == 4
+        assert (mod.RANK, mod.N_RANKS) == (mg.RANK, mg.N_RANKS)
 
 
 def test_metrics_and_profiling(tmp_path):
