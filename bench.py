@@ -124,6 +124,9 @@ def time_placement(placement, args, comm, dev, sync):
 
     for _ in range(args.warmup):
         engine.step()
+    # the last warmup step's pending (pipelined) update is applied before the clock starts,
+    # so the timed region holds exactly K forwards and K updates (the K-th one in drain())
+    engine.drain()
     loss0 = engine.last_loss()
     sync()
     comm.barrier()
