@@ -166,6 +166,54 @@ class FusedAdamEngine:
     def setup(self, guess, nsteps: int, param_bounds=None, learning_rate: float = 0.01,
               b1: float = 0.9, b2: float = 0.999, eps: float = 1e-8, history="full",
               legacy_bounds_jacobian: bool = False):
+        """Allocate the device state for ``nsteps`` steps from ``guess`` (collective).
+
+        Hashed placement on several GPUs with the two-shot exchange and no explicit chunk
+        count: the two-chunk layout (whose exchange may overlap the VJP on a side stream) is
+        timed against one chunk (one cross-rank rendezvous per step instead of two), and
+        the faster is kept -- both by the same setup-time measurement as the rest of the
+        schedule (:meth:`_autotune`)."""
+        kw = dict(param_bounds=param_bounds, learning_rate=learning_rate, b1=b1, b2=b2,
+                  eps=eps, history=history, legacy_bounds_jacobian=legacy_bounds_jacobian)
+        self._chunks_override = None
+        self._setup(guess, nsteps, **kw)
+        tun = self.tuning
+        if not (tun and self.twoshot is not None and not self.owner and self.C == 2
+                and not self._chunks_explicit and "ts_side" in tun["chosen"]):
+            return self
+        t2 = min(c["ms"] for c in tun["candidates"])
+        skip = getattr(self, "_skip_autotune", False)
+        self._chunks_override = 1
+        self._skip_autotune = True
+        try:
+            self._setup(guess, nsteps, **kw)
+        finally:
+            self._skip_autotune = skip
+        cands = [{"ts_side": False, "rccl_exchange": False}]
+        if os.environ.get("MULTIGRAD_HASHED_EXCHANGE", "auto").strip().lower() != "twoshot":
+            cands.append({"ts_side": False, "rccl_exchange": True})
+        self._autotune(cands, min_window_s=1e-3 * float(
+            os.environ.get("MULTIGRAD_AUTOTUNE_WINDOW_MS", "30")))
+        t1 = min(c["ms"] for c in self.tuning["candidates"])
+        chunk_times = {"1": t1, "2": t2}
+        if t1 <= t2:
+            self.tuning["chunks"] = dict(chunk_times, chosen=1)
+            return self
+        self._chunks_override = 2
+        self._skip_autotune = True
+        try:
+            self._setup(guess, nsteps, **kw)
+        finally:
+            self._skip_autotune = skip
+        for k, v in tun["chosen"].items():
+            setattr(self, k, v)
+        self.graph = None
+        self.tuning = dict(tun, chunks=dict(chunk_times, chosen=2))
+        return self
+
+    def _setup(self, guess, nsteps: int, param_bounds=None, learning_rate: float = 0.01,
+               b1: float = 0.9, b2: float = 0.999, eps: float = 1e-8, history="full",
+               legacy_bounds_jacobian: bool = False):
         md = self.model
         dev = md.param_device()
         self.device = dev
@@ -188,7 +236,8 @@ class FusedAdamEngine:
                 # two-shot: 2 chunks by default when the overlapped schedule may be chosen
                 # (side stream auto), else 1 -- each chunk is one more cross-rank rendezvous
                 side_mode = _side_stream_mode()
-                nch = self.nchunks_req if self._chunks_explicit else (2 if side_mode == "auto" else 1)
+                nch = self._chunks_override or (
+                    self.nchunks_req if self._chunks_explicit else (2 if side_mode == "auto" else 1))
                 ub, pb, P_pad, lengths = plan_chunks(J, upp, W, nch)
                 self.twoshot = self._connect_twoshot(P_pad)  # collective
             if self.twoshot is None:
