@@ -319,8 +319,10 @@ def run_lbfgs_device(loss_and_grad_fn: Callable, params, maxsteps: int = 100, pa
 def lbfgs_minimize(*args, **kwargs):
     """See ``_lbfgs_minimize_impl``; runs with the BLAS pools limited to one thread (the host-side
     compact-form solves are tiny; a spinning BLAS pool would slow the CPU evaluations)."""
+    from ..utils.hooks import driver_guard
     from ..utils.tensors import blas_single_thread
-    with blas_single_thread():
+    obj = args[0] if args else kwargs.get("obj")
+    with driver_guard(getattr(obj, "comm", None)), blas_single_thread():
         return _lbfgs_minimize_impl(*args, **kwargs)
 
 

@@ -185,6 +185,9 @@ def _lbfgsb_minimize_impl(obj, lo=None, hi=None, maxiter: int = 100, m: int = 10
     def allmax(a):
         return _allreduce_np(comm, np.asarray(a, dtype=np.float64), op="max", sharded=sharded)
 
+    from ..utils.hooks import StepHooks
+    hooks = StepHooks(comm, what="L-BFGS-B iterate")  # MULTIGRAD_CHECK_EVERY / _METRICS
+
     for k in range(maxiter + 1):
         # ------------------------------------------------ copy A: pair dots + GCP inputs
         t = torch.where(g < 0, (x - hi) / g, torch.where(g > 0, (x - lo) / g,
@@ -324,6 +327,8 @@ def _lbfgsb_minimize_impl(obj, lo=None, hi=None, maxiter: int = 100, m: int = 10
         pending = q
         nit = k + 1
         f_old, f, g = f, f_new, g_new
+        if hooks.active:
+            hooks(k, f, None, (lambda: x) if not sharded else None, nfev=nfev)
         if (f_old - f) <= ftol * max(abs(f_old), abs(f), 1.0):
             status, message = 0, "CONVERGENCE: REL_REDUCTION_OF_F_<=_FACTR*EPSMCH"
             if callback is not None:
@@ -538,8 +543,10 @@ def bounds_arrays(param_bounds, n: int):
 def lbfgsb_minimize(*args, **kwargs):
     """See ``_lbfgsb_minimize_impl``; runs with the BLAS pools limited to one thread (the host-side
     compact-form solves are tiny; a spinning BLAS pool would slow the CPU evaluations)."""
+    from ..utils.hooks import driver_guard
     from ..utils.tensors import blas_single_thread
-    with blas_single_thread():
+    obj = args[0] if args else kwargs.get("obj")
+    with driver_guard(getattr(obj, "comm", None)), blas_single_thread():
         return _lbfgsb_minimize_impl(*args, **kwargs)
 
 
