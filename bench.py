@@ -77,13 +77,35 @@ def _free_port() -> int:
         return int(s.getsockname()[1])
 
 
+def visible_gpus() -> int:
+    """GPUs this process could use, counted without touching the GPU runtime (no torch, no
+    HIP call): the first ``*_VISIBLE_DEVICES`` list that is set, else the KFD topology nodes
+    with a non-zero ``gpu_id`` (CPU nodes have 0).  0 if nothing is visible."""
+    for var in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            return len([d for d in v.split(",") if d.strip() not in ("", "-1")])
+    base = "/sys/class/kfd/kfd/topology/nodes"
+    n = 0
+    try:
+        for node in os.listdir(base):
+            try:
+                with open(os.path.join(base, node, "gpu_id")) as f:
+                    n += int(f.read().strip() or 0) != 0
+            except (OSError, ValueError):
+                pass
+    except OSError:
+        return 0
+    return n
+
+
 def launch(args, argv) -> int:
     """Start ``args.gpus`` ranks with torch.distributed.run and relay their output.
 
-    Runs in a process that has made no GPU call (device counting does not initialise
-    the runtime), and starts the ranks as children -- never exec."""
-    import torch
-    ndev = torch.cuda.device_count()
+    GPU-free by construction: this parent process imports no torch and makes no HIP call
+    (GPUs are counted from the environment / sysfs), and it starts the ranks as children
+    -- never exec."""
+    ndev = visible_gpus()
     if 0 < ndev < args.gpus:
         print(f"bench.py: --gpus {args.gpus} requested but only {ndev} GPU(s) are visible",
               file=sys.stderr, flush=True)

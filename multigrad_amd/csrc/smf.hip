@@ -795,6 +795,184 @@ __device__ __forceinline__ void lane_halo_ep(float x0, float x1, float ninv, flo
   }
 }
 
+// ---------------------------------------------------------- Euler-Maclaurin bin masses
+// MG_FWD_EM (absolute contract, uniformly spaced edges): inside a lanes group every halo of
+// a lane shares the lane's sigma, so the bin width in sigma units h = delta / sigma is a
+// lane constant.  The mass of bin k is then the integral of the Gaussian over one panel of
+// width h, evaluated by the Euler-Maclaurin formula from the Gaussian factor and its odd
+// derivatives at the two edges (f = exp(-z^2/2), f' = -z f, f''' = (3z - z^3) f,
+// f^(5) = -(z^5 - 10 z^3 + 15 z) f):
+//   mass_k = (h/2)(f_k + f_{k+1}) + [E]_k^{k+1},   E(z) = f z (c1 + c3 z^2 + c5 z^4)
+//   c1 = h^2/12 + 3h^4/720 + 15h^6/30240,  c3 = -(h^4/720 + 10h^6/30240),  c5 = h^6/30240
+// (all over sqrt(2 pi)).  The remainder is h^9 B_8/8! f^(8) <= 3.5e-5 h^9: 6.8e-8 absolute at
+// the largest width the path accepts (kEmHMax = 0.5, about the float32 erf of the
+// reference), far below the argument rounding of any per-edge evaluation.
+// The Gaussian factors of the NB+1 equally spaced edges come from ONE seed pair per halo by
+// the exact recurrence f_{e+2} = f_e exp2(-4 dw w_{e+1}) (w = z * kWScale, dw = edge spacing
+// in w): the seed pair (edges 2M, 2M+1, M = NP/2) and R = exp2(-4 dw w_{2M+1}) are three
+// v_exp and one v_rcp per halo; pair M+j is p_j = (f_2M, f_2M+1) R^j, exact up to the lane
+// constant Q_j = (exp2(-4 dw^2 j(j-1)), exp2(-4 dw^2 j^2)), which is applied to the per-group
+// sums once per group instead of per halo.  Every per-edge sum the forward needs -- the trap
+// part F = sum f, E = sum E(w), and the VJP residuals G = F, W = sum f w -- is linear in f, so
+// a halo costs 9 packed ops per edge pair and no per-edge transcendental, no v_rcp and no
+// sign / count bookkeeping: 4 v_exp/v_rcp per halo against 22 for the rational tail.
+// A group whose lanes are not all inside kEmHMax (or non-uniform / padded bins, or the
+// relative-tail contract) runs the per-edge tail evaluation instead (the ballot is
+// wave-uniform).  The VJP residuals agree with the per-edge exponentials to the chain's
+// rounding (~1e-6 relative), inside the VJP's contract.
+#ifndef MG_FWD_EM
+#define MG_FWD_EM 1
+#endif
+constexpr float kEmHMax = 0.5f;
+constexpr float kInvSqrt2Pi = 0.39894228040143268f;
+
+struct EmLane {
+  float inv;         // kWScale / sigma
+  float dw4;         // -4 dw
+  float a1, a3, a5;  // E(w) = f w (a1 + a3 w^2 + a5 w^4)  (w units)
+};
+
+__device__ __forceinline__ EmLane em_lane(float inv, float delta) {
+  constexpr float ik = 1.0f / kWScale;
+  EmLane L;
+  L.inv = inv;
+  const float dw = delta * inv;
+  L.dw4 = -4.0f * dw;
+  const float h = dw * ik;
+  const float h2 = h * h, h4 = h2 * h2, h6 = h4 * h2;
+  L.a1 = (h2 * (1.0f / 12.0f) + h4 * (3.0f / 720.0f) + h6 * (15.0f / 30240.0f)) * ik;
+  L.a3 = -(h4 * (1.0f / 720.0f) + h6 * (10.0f / 30240.0f)) * (ik * ik * ik);
+  L.a5 = h6 * (1.0f / 30240.0f) * (ik * ik * ik * ik * ik);
+  return L;
+}
+
+// One halo (nm = -(x + a) inv): F, Wa, E accumulate the UNSCALED sums of edge pairs (the
+// pair layout of EdgePairs; an odd last edge in the .x half of the extra pair).
+template <int NB, bool RESID>
+__device__ __forceinline__ void em_halo(float nm, const EmLane& L, const SmfBins& b,
+                                        v2f (&F)[EdgePairs<NB>::NV], v2f (&Wa)[EdgePairs<NB>::NV],
+                                        v2f (&E)[EdgePairs<NB>::NV]) {
+  using EP = EdgePairs<NB>;
+  constexpr int M = EP::NP / 2;
+  // sentinel / masked halos (x = -1e30 or -inf): f = 0, and w^4 stays finite so 0 * E = 0
+  nm = __builtin_amdgcn_fmed3f(nm, -1e6f, 1e6f);
+  // w of the seed pair from the edges; the other pairs step by 2 dw (two lane constants
+  // instead of one per pair, which the compiler would otherwise keep in registers)
+  const float dw2 = -0.5f * L.dw4;
+  v2f wm;
+  {
+    v2f e2;
+    e2.x = b.edge[2 * M];
+    e2.y = b.edge[2 * M + 1];
+    wm = e2 * L.inv + nm;
+  }
+  auto wpair = [&](int i) { return wm + (float)(i - M) * dw2; };
+  auto accum = [&](int i, v2f p, v2f w) {
+    const v2f pw = p * w;
+    F[i] = F[i] + p;
+    if constexpr (RESID) Wa[i] = Wa[i] + pw;
+    const v2f w2 = w * w;
+    v2f t = w2 * L.a5 + L.a3;
+    t = t * w2 + L.a1;
+    E[i] = pw * t + E[i];
+  };
+  const v2f ws = wpair(M);
+  const v2f q = -ws * ws;
+  v2f p0;
+  p0.x = fast_exp2(q.x);
+  p0.y = fast_exp2(q.y);
+  const float R = fast_exp2(__builtin_amdgcn_fmed3f(L.dw4 * ws.y, -126.0f, 126.0f));
+  accum(M, p0, ws);
+  v2f p = p0;
+#pragma unroll
+  for (int i = M + 1; i < EP::NP; ++i) {
+    p = p * R;
+    accum(i, p, wpair(i));
+  }
+  if constexpr (EP::NX) {  // odd last edge: scalar (a packed op costs two scalar issues anyway)
+    const float pz = p.x * R;
+    const float wz = fmaf((float)(EP::NP - M), dw2, wm.x);
+    const float pw = pz * wz;
+    F[EP::NP].x += pz;
+    if constexpr (RESID) Wa[EP::NP].x += pw;
+    const float w2 = wz * wz;
+    const float t = fmaf(fmaf(w2, L.a5, L.a3), w2, L.a1);
+    E[EP::NP].x = fmaf(pw, t, E[EP::NP].x);
+  }
+  if constexpr (M > 0) {
+    const float Ri = fast_rcp(R);
+    p = p0;
+#pragma unroll
+    for (int i = M - 1; i >= 0; --i) {
+      p = p * Ri;
+      accum(i, p, wpair(i));
+    }
+  }
+}
+
+// MG_EM_SCHED_BARRIER: keep the scheduler from interleaving consecutive halos (their
+// temporaries would double the register footprint of the pipelined-update kernel)
+#ifndef MG_EM_SCHED_BARRIER
+#define MG_EM_SCHED_BARRIER 1
+#endif
+template <int NB, bool RESID>
+__device__ __forceinline__ void lane_halo_em(float x, const EmLane& L, float nma,
+                                             const SmfBins& b, v2f (&F)[EdgePairs<NB>::NV],
+                                             v2f (&Wa)[EdgePairs<NB>::NV],
+                                             v2f (&E)[EdgePairs<NB>::NV]) {
+  em_halo<NB, RESID>(fmaf(x, -L.inv, nma), L, b, F, Wa, E);
+#if MG_EM_SCHED_BARRIER
+  __builtin_amdgcn_sched_barrier(0);
+#endif
+}
+
+// End of a group: apply the lane constants Q_j to the pair sums (F, Wa become the true
+// residuals G, W), and add the lane's cumulative bin masses C_e (C_{k+1} - C_k = mass_k) to
+// the per-edge accumulators of the edge-pair path.
+template <int NB>
+__device__ __forceinline__ void em_group_end(const EmLane& L, v2f (&F)[EdgePairs<NB>::NV],
+                                             v2f (&Wa)[EdgePairs<NB>::NV],
+                                             v2f (&E)[EdgePairs<NB>::NV],
+                                             v2f (&accp)[EdgePairs<NB>::NV]) {
+  using EP = EdgePairs<NB>;
+  constexpr int M = EP::NP / 2;
+  const float l4 = 0.25f * L.dw4 * L.dw4;  // 4 dw^2 ... as -(dw4^2)/4 = -4 dw^2 below
+#pragma unroll
+  for (int i = 0; i < EP::NV; ++i) {
+    const int j = i - M;
+    v2f Q;
+    Q.x = (j * (j - 1) == 0) ? 1.0f : fast_exp2(-l4 * (float)(j * (j - 1)));
+    Q.y = (i == EP::NP) ? Q.x : ((j * j == 0) ? 1.0f : fast_exp2(-l4 * (float)(j * j)));
+    F[i] = F[i] * Q;
+    Wa[i] = Wa[i] * Q;
+    E[i] = E[i] * Q;
+  }
+  // trapezoid weight h/2 and the normalisation, in w units: h = dw / kWScale
+  const float hh = (-0.125f / kWScale) * L.dw4;  // dw / (2 kWScale)
+  float T = 0.0f, fprev = 0.0f;
+#pragma unroll
+  for (int e = 0; e <= NB; ++e) {
+    const int i = e >> 1;
+    float fe, ee;
+    if (i < EP::NP) {
+      fe = (e & 1) ? F[i].y : F[i].x;
+      ee = (e & 1) ? E[i].y : E[i].x;
+    } else {
+      fe = F[i].x + F[i].y;
+      ee = E[i].x + E[i].y;
+    }
+    if (e > 0) T = fmaf(hh, fprev + fe, T);
+    fprev = fe;
+    const float C = kInvSqrt2Pi * (T + ee);
+    if (i < EP::NP) {
+      if (e & 1) accp[i].y += C;
+      else accp[i].x += C;
+    } else {
+      accp[i].x += C;
+    }
+  }
+}
+
 // Measured on MI355X (1e7 params, 1.34e8 halos, internal order, with residuals): the
 // edge-pair path at 4 waves/SIMD (118 VGPRs, no spills) 595 us vs 615-624 us for the
 // compiler-packed scalar path at 6 waves; at 5 or 6 waves the edge-pair path spills.
@@ -944,6 +1122,7 @@ __global__ __launch_bounds__(kThreads, MG_LANES_MINWAVES) void smf_fwd_lanes_ker
   // the pipelined update's staging buffer (LDS budget of 4 workgroups per CU)
   constexpr int kRepl =
       (!REL && MG_LANES_EP && (MG_FWD_TAB >= 2 || (MG_FWD_TAB == 1 && !RESID))) ? (UPD ? 8 : 16) : 0;
+  constexpr bool kEm = MG_FWD_EM && MG_LANES_EP && !REL;
   const float4* tb = nullptr;
   if constexpr (kRepl > 0) {
     __shared__ float4 tab[kTailTabN * (kRepl > 0 ? kRepl : 1)];
@@ -1166,8 +1345,41 @@ __global__ __launch_bounds__(kThreads, MG_LANES_MINWAVES) void smf_fwd_lanes_ker
       W[e] = 0.0f;
     }
 #endif
+    // Euler-Maclaurin path (see em_halo) when every occupied lane's bin width is inside
+    // kEmHMax; the ballot makes the choice wave-uniform
+    bool em = false;
+#if MG_LANES_EP
+    if constexpr (kEm) {
+      const float inv = -ninv;
+      const bool bad = c_cur >= 0 && !(bins.delta * inv * (1.0f / kWScale) <= kEmHMax);
+      em = bins.delta > 0.0f && __builtin_amdgcn_ballot_w64(bad) == 0;
+    }
+    if constexpr (kEm) if (em) {
+      const EmLane eml = em_lane(-ninv, bins.delta);
+      v2f Ep[EP::NV];
+#pragma unroll
+      for (int e = 0; e < EP::NV; ++e) Ep[e] = (v2f)(0.0f);
+      for (int j = 0; j < len; j += kLanesUnroll) {
+        float xc[kLanesUnroll];
+#pragma unroll
+        for (int u = 0; u < kLanesUnroll; ++u) {
+          xc[u] = lane_use(xn[u], j + u, len);
+          xn[u] = lane_load(xp, j + kLanesUnroll + u, len);
+        }
+#pragma unroll
+        for (int u = 0; u < kLanesUnroll; ++u)
+          lane_halo_em<NB, RESID>(xc[u], eml, -mua, bins, Gp, Wp, Ep);
+      }
+      em_group_end<NB>(eml, Gp, Wp, Ep, accp);
+    }
+#endif
     // the next kLanesUnroll loads are in flight while the current halos are computed;
     // past-the-end halos are the sentinel (exact zero contribution)
+#ifdef MG_FWD_EM_ONLY
+    if (!kEm)
+#else
+    if (!em)
+#endif
     for (int j = 0; j < len; j += kLanesUnroll) {
       float xc[kLanesUnroll];
 #pragma unroll

@@ -185,3 +185,25 @@ def test_bench_self_launches_n_ranks():
     assert rec["config"]["optimizer_sharding"] == "zero1"
     assert rec["owner_steps_per_s"] > 0
     assert rec["owner_config"]["optimizer_sharding"] == "owner"
+
+
+def test_bench_launcher_parent_is_gpu_free():
+    """The parent that starts the ranks imports no torch (so it cannot initialise HIP) and
+    counts GPUs from the environment / sysfs."""
+    code = ("import sys, bench\n"
+            "seen = []\n"
+            "class R: returncode = 0\n"
+            "bench.subprocess.run = lambda cmd, env=None: (seen.append(cmd), R)[1]\n"
+            "rc = bench.main(['--gpus', '2', '--steps', '1'])\n"
+            "assert rc == 0 and seen and 'torch.distributed.run' in seen[0], seen\n"
+            "assert 'torch' not in sys.modules, 'launcher imported torch'\n"
+            "import os\n"
+            "os.environ['HIP_VISIBLE_DEVICES'] = '0,1,2'\n"
+            "assert bench.visible_gpus() == 3\n"
+            "print('ok')\n")
+    env = dict(os.environ, HIP_VISIBLE_DEVICES="0,1")
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, "-c", code], cwd=ROOT, env=env, capture_output=True,
+                       text=True, timeout=120)
+    assert r.returncode == 0 and r.stdout.strip() == "ok", r.stderr[-2000:]
