@@ -926,6 +926,44 @@ __device__ __forceinline__ void lane_halo_em(float x, const EmLane& L, float nma
 #endif
 }
 
+// Per-edge evaluation of ONE halo (absolute contract, scalar) into the edge-pair
+// accumulators: the fallback of the Euler-Maclaurin kernels for groups outside kEmHMax.
+// It is deliberately lean in registers (one halo, one edge at a time): with the packed
+// two-halo path as the fallback the pipelined-update kernel spilled 33 VGPRs and ran 12%
+// slower even though no group took the fallback (profiles/em_forward/).
+template <int NB, bool RESID>
+__device__ __forceinline__ void lane_halo_exact1(float x, float ninv, float mua, const SmfBins& b,
+                                                 v2f (&acc)[EdgePairs<NB>::NV], int (&cnt)[NB + 1],
+                                                 v2f (&G)[EdgePairs<NB>::NV],
+                                                 v2f (&W)[EdgePairs<NB>::NV]) {
+  const float mu = fmaf(x, -ninv, mua);
+#pragma unroll
+  for (int e = 0; e <= NB; ++e) {
+    const float n = fmaf(b.edge[e], ninv, mu);
+    float p, g;
+    normal_tail_parts_w<false>(n, p, g);
+    const float v = p * __builtin_copysignf(g, n);
+    cnt[e] += __builtin_popcountll(__builtin_amdgcn_ballot_w64(n < 0.0f));
+    const int i = e >> 1;
+    if (e & 1) {
+      acc[i].y += v;
+      if constexpr (RESID) {
+        G[i].y += g;
+        W[i].y = fmaf(-g, n, W[i].y);
+      }
+    } else {
+      acc[i].x += v;
+      if constexpr (RESID) {
+        G[i].x += g;
+        W[i].x = fmaf(-g, n, W[i].x);
+      }
+    }
+  }
+#if MG_EM_SCHED_BARRIER
+  __builtin_amdgcn_sched_barrier(0);
+#endif
+}
+
 // End of a group: apply the lane constants Q_j to the pair sums (F, Wa become the true
 // residuals G, W), and add the lane's cumulative bin masses C_e (C_{k+1} - C_k = mass_k) to
 // the per-edge accumulators of the edge-pair path.
@@ -1121,7 +1159,8 @@ __global__ __launch_bounds__(kThreads, MG_LANES_MINWAVES) void smf_fwd_lanes_ker
   // signed-tail table (absolute contract): 16 replicas (conflict-free reads), 8 next to
   // the pipelined update's staging buffer (LDS budget of 4 workgroups per CU)
   constexpr int kRepl =
-      (!REL && MG_LANES_EP && (MG_FWD_TAB >= 2 || (MG_FWD_TAB == 1 && !RESID))) ? (UPD ? 8 : 16) : 0;
+      (!REL && MG_LANES_EP && !(MG_FWD_EM) && (MG_FWD_TAB >= 2 || (MG_FWD_TAB == 1 && !RESID)))
+          ? (UPD ? 8 : 16) : 0;  // (with MG_FWD_EM the fallback is the lean per-edge path)
   constexpr bool kEm = MG_FWD_EM && MG_LANES_EP && !REL;
   const float4* tb = nullptr;
   if constexpr (kRepl > 0) {
@@ -1389,10 +1428,16 @@ __global__ __launch_bounds__(kThreads, MG_LANES_MINWAVES) void smf_fwd_lanes_ker
         xn[u] = lane_load(xp, jn, len);
       }
 #if MG_LANES_EP
+      if constexpr (kEm) {  // lean fallback of the Euler-Maclaurin kernels
 #pragma unroll
-      for (int u = 0; u < kLanesUnroll; u += 2)
-        lane_halo_ep<NB, LOGSIG, REL, RESID, kRepl>(xc[u], xc[u + 1], ninv, mua, bins, accp, cnt,
-                                                    Gp, Wp, tb);
+        for (int u = 0; u < kLanesUnroll; ++u)
+          lane_halo_exact1<NB, RESID>(xc[u], ninv, mua, bins, accp, cnt, Gp, Wp);
+      } else {
+#pragma unroll
+        for (int u = 0; u < kLanesUnroll; u += 2)
+          lane_halo_ep<NB, LOGSIG, REL, RESID, kRepl>(xc[u], xc[u + 1], ninv, mua, bins, accp,
+                                                      cnt, Gp, Wp, tb);
+      }
 #elif MG_LANES_V2
       static_assert(kLanesUnroll % 2 == 0, "packed path takes halo pairs");
 #pragma unroll

@@ -474,3 +474,106 @@ def test_forward_schedules_at_eighth_shard_vs_fp64(monkeypatch, mode):
     (g64,) = torch.autograd.grad((torch.special.ndtr(z) * hw[None, :]).sum(), t64)
     np.testing.assert_allclose(grad[:2 * npop_s].cpu().double(), g64.cpu(), rtol=2e-4,
                                atol=2e-5 * float(g64.abs().max()))
+
+
+def _narrow_guess(data, every=2, logsig=-1.7):
+    """The population guess with log10 sigma = ``logsig`` on every ``every``-th population:
+    bin width / sigma = 5 there, far outside the Euler-Maclaurin path's kEmHMax = 0.5, so
+    most lanes groups mix both kinds of lane and take the per-edge fallback."""
+    g = data["guess"].clone()
+    g[1::2 * every] = logsig
+    return g
+
+
+def test_em_forward_fallback_groups_vs_fp64():
+    """Lanes forward with residuals where many groups must take the per-edge fallback
+    (narrow populations) and the rest the Euler-Maclaurin path: sumstats against the fp64
+    oracle, residual VJP against autograd of the oracle."""
+    from multigrad_amd.models.population import make_population_data
+    data = make_population_data(num_params=20_000, num_halos=600_000, seed=5, device=DEV)
+    shard, bins = data["shard"], data["bins"]
+    th = _narrow_guess(data)
+    out = torch.zeros(bins.nbp, device=DEV)
+    S.smf_forward_into(th, shard, bins, True, out, resid=True)
+    ref = S.smf_sumstats_reference(th.double(), shard.x.double(), shard.pop, bins, True)
+    np.testing.assert_allclose(out[:bins.nb].cpu().double(), ref.cpu(), rtol=2e-5)
+    h = torch.linspace(0.6, -0.5, bins.nbp + 1, device=DEV)
+    grad = torch.zeros_like(th)
+    S.smf_vjp_into(th, shard, bins, True, h, grad, residuals_ready=True)
+    t64 = th.double().clone().requires_grad_(True)
+    hw = h[:bins.nb + 1].double() * np.sqrt(2 * np.pi)
+    t2 = t64.reshape(-1, 2)
+    p = shard.pop.long()
+    mu = shard.x.double() + t2[:, 0][p]
+    sig = torch.pow(10.0, t2[:, 1][p])
+    z = (torch.tensor(bins.edges, dtype=torch.float64, device=DEV)[None, :] - mu[:, None]) / sig[:, None]
+    (g64,) = torch.autograd.grad((torch.special.ndtr(z) * hw[None, :]).sum(), t64)
+    np.testing.assert_allclose(grad.cpu().double(), g64.cpu(), rtol=2e-4,
+                               atol=2e-5 * float(g64.abs().max()))
+
+
+def test_pipelined_update_with_fallback_groups_matches_unpipelined(monkeypatch):
+    """The pipelined-update forward (Euler-Maclaurin + fallback groups in one launch) gives
+    the step-by-step engine's trajectory."""
+    from multigrad_amd.engine.fused import FusedAdamEngine
+    from multigrad_amd.models.population import PopulationSMFModel, make_population_data
+    data = make_population_data(num_params=6000, num_halos=300_000, seed=12, device=DEV)
+    model = PopulationSMFModel(aux_data=data)
+    model.set_target_from_truth()
+    guess = _narrow_guess(data, every=3)
+    monkeypatch.setenv("MULTIGRAD_PIPELINE", "0")
+    ref = FusedAdamEngine(model, graph=False).run_adam(guess, nsteps=5, learning_rate=1e-3)
+    monkeypatch.setenv("MULTIGRAD_PIPELINE", "1")
+    eng = FusedAdamEngine(model, graph=False)
+    t = eng.run_adam(guess, nsteps=5, learning_rate=1e-3)
+    assert eng.pipeline
+    torch.testing.assert_close(t, ref, rtol=1e-6, atol=1e-7)
+
+
+def test_headline_kernel_vs_fp64(monkeypatch):
+    """The exact timed instantiation -- smf_fwd_lanes_kernel<10,true,false,true,true>, the
+    pipelined forward with the fused VJP + Adam, at the headline size (1e7 parameters,
+    1.34e8 halos) -- for 2 steps: S(theta_1) against the fp64 oracle (rtol 2e-5), and the
+    step-0 gradient (read back from the first Adam moment, m = (1 - b1) g) on 2000
+    populations against autograd of the fp64 loss (rtol 2e-4)."""
+    from multigrad_amd.engine.fused import FusedAdamEngine
+    from multigrad_amd.models.population import PopulationSMFModel, make_population_data
+    from multigrad_amd.ops.smf import logmse_loss
+    monkeypatch.setenv("MULTIGRAD_PIPELINE", "1")
+    monkeypatch.setenv("MULTIGRAD_AUTOTUNE", "0")
+    data = make_population_data(num_params=10_000_000, num_halos=1 << 27, seed=1234, device=DEV)
+    model = PopulationSMFModel(aux_data=data)
+    model.set_target_from_truth()
+    shard, bins = data["shard"], data["bins"]
+    eng = FusedAdamEngine(model, graph=False)
+    # more steps than are taken: the last step of a run drains its pending update
+    eng.setup(data["guess"], nsteps=4, learning_rate=1e-3, history="last")
+    assert eng.pipeline and shard.layout == "lanes"
+    eng.step()
+    eng.step()           # applies update 0 in the forward, evaluates S(theta_1)
+    torch.cuda.synchronize()
+    theta1 = eng.to_user(eng.theta[:eng.P]).clone()
+    S1 = eng.S[:bins.nb].double().cpu()
+    g0 = (eng.to_user(eng.m[:eng.P]) / (1.0 - eng.b1)).double()
+    th0 = data["guess"].double()
+
+    def oracle(th64, sel=None):
+        tot = torch.zeros(bins.nb, dtype=torch.float64, device=DEV)
+        for a in range(0, shard.n, 1 << 22):
+            tot += S.smf_sumstats_reference(th64, shard.x[a:a + (1 << 22)].double(),
+                                            shard.pop[a:a + (1 << 22)], bins, True)
+        return tot
+
+    ref1 = oracle(theta1.double())
+    np.testing.assert_allclose(S1, ref1.cpu(), rtol=2e-5)
+    # dL/dS at theta_0 from the fp64 sumstats, then the gradient of the populations < 2000
+    S0 = oracle(th0).requires_grad_(True)
+    t = data["target_sumstats"].double()
+    (dLdS,) = torch.autograd.grad(logmse_loss(S0, t, data["loss_eps"]), S0)
+    npop_s = 2000
+    sel = shard.pop < npop_s
+    t64 = th0[:2 * npop_s].clone().requires_grad_(True)
+    part = S.smf_sumstats_reference(t64, shard.x[sel].double(), shard.pop[sel], bins, True)
+    (gref,) = torch.autograd.grad(part, t64, dLdS)
+    np.testing.assert_allclose(g0[:2 * npop_s].cpu(), gref.cpu(), rtol=2e-4,
+                               atol=2e-5 * float(gref.abs().max()))
