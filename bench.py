@@ -196,6 +196,7 @@ def time_placement(placement, args, comm, dev, sync):
     }
     if args.profile_phases:
         info["phases_ms"] = {k: round(v, 4) for k, v in engine.timer.summary().items()}
+    engine.close()  # the two-shot context goes back to the communicator's pool
     del engine, model, data
     if dev.type == "cuda":
         torch.cuda.synchronize()
@@ -304,6 +305,11 @@ def main(argv=None):
         "loss_last": head["loss_last"],
         "setup_s": head["setup_s"],
     }
+    if comm.size > 1:
+        # connect-time verdicts of the peer-memory collectives: stress self-test passed
+        # (back-to-back device-only exchanges) or the RCCL fallback and why
+        from multigrad_amd.parallel.xgmi import status
+        rec["peer_memory_selftest"] = status(comm)
     if errors:
         rec["errors"] = errors
     if own is not None and own is not head:

@@ -146,6 +146,7 @@ class FusedAdamEngine:
         # two-shot xGMI reduce-scatter -> Adam -> all-gather of the dense gradient (ZeRO
         # mode on GPUs; parallel/xgmi.py): None = RCCL collectives
         self.twoshot = None
+        self._ts_keep = None  # the acquired two-shot context (kept across setups)
         nc = chunks if chunks is not None else int(os.environ.get("MULTIGRAD_CHUNKS", "0")) or None
         self._chunks_explicit = nc is not None
         self.nchunks_req = nc if nc is not None else (1 if self.size == 1 else 4)
@@ -533,17 +534,29 @@ class FusedAdamEngine:
     def _connect_twoshot(self, numel: int):
         """The two-shot context for ``numel`` floats (kept across setups of the same
         size), connecting it now if needed -- collective; None: use RCCL."""
-        from ..parallel.xgmi import connect_twoshot, twoshot_enabled
+        from ..parallel.xgmi import acquire_twoshot, release_twoshot, twoshot_enabled
         if not twoshot_enabled() or self.size > 8:
             return None
-        ts = self.twoshot
+        ts = self._ts_keep
         if ts is not None:
             torch.cuda.synchronize()  # no exchange of a previous run still in flight
         if ts is not None and ts.numel == numel:
             return ts
         if ts is not None:
-            ts.close()
-        return connect_twoshot(self.comm, numel)
+            release_twoshot(self.comm, ts)
+            self._ts_keep = None
+        self._ts_keep = acquire_twoshot(self.comm, numel)
+        return self._ts_keep
+
+    def close(self) -> None:
+        """Give the engine's peer-memory exchange context back to the communicator's pool
+        (collective: every rank closes its engine).  The engine cannot step afterwards."""
+        from ..parallel.xgmi import release_twoshot
+        if getattr(self, "_ts_keep", None) is not None:
+            release_twoshot(self.comm, self._ts_keep)
+        self._ts_keep = None
+        self.twoshot = None
+        self.ready = False
 
     def _twoshot_update(self, c: int):
         """Chunk c: dense-gradient reduce-scatter + Adam on the owned slice + all-gather,
@@ -888,7 +901,8 @@ class FusedAdamEngine:
         if self.owner:
             a, b = self.own_range
             return self.to_user(self._assemble(self.theta[a:b]))
-        return self.to_user(self.theta[:self.P])
+        # a copy: theta may be the peer-memory region a later engine reuses
+        return self.to_user(self.theta[:self.P]).clone()
 
     def last_loss(self) -> float:
         loss = float(self.loss.item())
@@ -1044,8 +1058,9 @@ class FusedAdamEngine:
 
     def load_checkpoint(self, path: str) -> int:
         from ..utils import checkpoint as ckpt
-        return self.load_state_dict(ckpt.load_optimizer_state(path, rank=self.rank,
-                                                              sharded=self.sharded))
+        return self.load_state_dict(ckpt.load_optimizer_state(
+            path, rank=self.rank, sharded=self.sharded,
+            comm=self.comm if self.size > 1 and self.sharded else None))
 
     # ------------------------------------------------------------------ driver
     def run_adam(self, guess, nsteps: int = 100, param_bounds=None, learning_rate: float = 0.01,

@@ -1,4 +1,4 @@
-"""Graph-captured Adam engine for ANY torch ``OnePointModel``.
+"""Graph-captured Adam engine for ANY torch ``OnePointModel`` or ``OnePointGroup``.
 
 The reference's distributed chain rule works for every user model
 (multigrad/multigrad.py:508-538) and its Adam loop is ``jax.example_libraries`` Adam
@@ -9,26 +9,49 @@ step of a user model -- its autograd forward, the sumstat all-reduce, the loss c
 the VJP, the dense-gradient sum and the fused Adam update with the trajectory write --
 into a HIP graph, and replays it:
 
-    partial = calc_partial_sumstats_from_params(p)          # user hook, autograd
-    S = sum_ranks(partial)       one-shot xGMI kernel (<= 64 floats) | RCCL
-    cot = d loss(S) / dS                                    # user hook, autograd
+    partial = calc_partial_sumstats_from_params(p[, randkey])   # user hook, autograd
+    S = sum_ranks(partial)       one-shot xGMI kernel (<= 64 fp32) | RCCL
+    cot = d loss(S[, aux][, randkey]) / dS                      # user hook, autograd
     g = VJP(partial, p, cot)
     world 1:  fused Adam (bounded or not) + trajectory row  (csrc/adam.hip)
     world W:  two-shot kernel: reduce-scatter g -> Adam on the owned 1/W -> all-gather p
               (csrc/xgmi.hip), or RCCL all-reduce + fused Adam
 
-A step is replayable only if every collective in it is a peer-memory kernel with its
-sequence number on the device (one rank, or one-shot + two-shot) and the user hooks make
-no host synchronisation; the step counter lives on the device so replays self-advance.
-Anything else -- RCCL collectives, a capture error in user code, per-step PRNG keys --
-runs the same step eagerly (the reason is kept in ``fallback_reason``).  By default the
-engine times a few eager steps against a few replays and keeps the faster mode
-(``tuning``): replays remove the per-op launch cost but measured slower than eager
-launches once the step is GPU bound.
+What the reference API allows, the engine runs (reference multigrad/multigrad.py):
 
-The gradient exchange is one bucket after the VJP: a generic model consumes its
-parameters as one tensor, so autograd produces the whole gradient at once and there is
-nothing to overlap inside the VJP.
+* ``sumstats_func_has_aux`` (``:518-523``): the aux stays on its rank and goes to the loss
+  hook as its second argument, exactly as in the eager chain rule.
+* per-step ``randkey`` / ``const_randkey`` (``multigrad/adam.py:59-62``,
+  ``multigrad.py:289-300``): the keys follow the eager driver's sequence (one split per
+  step, the same on every rank).  Eager steps hand the hooks the step's key.  A captured
+  step hands them a capture key whose ``generator(device)`` returns a CUDA generator
+  registered with the graph; before each replay the engine seeds those generators with
+  the step's key, so a replay draws exactly what a fresh ``key.generator(device)`` would
+  (same Philox seed, offset 0).  Any other use of the key inside a hook (its integer
+  value, a split, a host generator) cannot be replayed and sends the run down the eager
+  path, decided collectively.
+* ``OnePointGroup`` (``:547-607``): each member's chain rule runs on its own
+  sub-communicator (one-shot sumstat sum per sub-communicator); every rank adds its local
+  VJPs, and the main communicator sums ``[grad]`` once -- the two-shot Adam exchange -- and
+  the group loss (each sub-communicator's rank 0 contributes its member's loss) with one
+  1-float one-shot exchange.  The reference all-reduces each member's gradient on its
+  sub-communicator and then all-gathers ``[loss, grad]`` over the main communicator; the
+  sum is the same, with one dense exchange instead of two.
+
+A step is replayable only if every collective in it is a peer-memory kernel with its
+sequence number on the device (one rank, or one-shot + two-shot) with fp32 sumstats of at
+most 64 values, and the user hooks make no host synchronisation; the step counter lives on
+the device so replays self-advance.  Anything else runs the same step eagerly (the reason
+is kept in ``fallback_reason``).  By default the engine times a few eager steps against a
+few replays and keeps the faster mode (``tuning``).
+
+On several ranks the two-shot exchange owns the parameters in peer memory (uncached); the
+hooks read a cached copy refreshed once per step (``p``), so a gather-heavy torch model
+does not read its parameters through uncached memory.
+
+The gradient exchange is one bucket after the VJP: the reference API gives a model ONE
+parameter array (multigrad/multigrad.py:482), so autograd delivers the whole gradient at
+once and there is nothing to overlap inside the VJP.
 """
 from __future__ import annotations
 
@@ -41,20 +64,52 @@ import torch
 from ..ops.adam import adam_step_
 from ..optim.adam import History
 from ..optim.transforms import Bounds
+from ..utils.random import PRNGKey, init_randkey
 from ..utils.tensors import as_param_tensor
 
-__all__ = ["GraphAdamEngine"]
+__all__ = ["GraphAdamEngine", "KeyNotCapturable"]
+
+
+class KeyNotCapturable(RuntimeError):
+    """A hook used its randkey in a way a graph replay cannot reproduce."""
+
+
+class _CaptureKey:
+    """The ``randkey`` the hooks see while a step is captured: only
+    ``generator(<cuda device>)`` is allowed (graph-registered, seeded before each replay)."""
+
+    dtype = "prng_key"
+
+    def __init__(self, eng: "GraphAdamEngine"):
+        object.__setattr__(self, "_eng", eng)
+
+    def generator(self, device="cpu") -> torch.Generator:
+        return self._eng._next_generator(device)
+
+    def __getattr__(self, name):
+        raise KeyNotCapturable(
+            f"randkey.{name} inside a captured step: only randkey.generator(<cuda device>) "
+            f"can be replayed with a fresh key per step")
+
+
+def _leaf_view(p: torch.Tensor, shape) -> torch.Tensor:
+    return p.detach().view(shape).requires_grad_(True)
 
 
 class GraphAdamEngine:
-    """Adam over a generic :class:`~multigrad_amd.models.onepoint.OnePointModel`.
+    """Adam over a generic :class:`~multigrad_amd.models.onepoint.OnePointModel` (or a
+    :class:`~multigrad_amd.models.onepoint.OnePointGroup` of them).
 
     ``graph``: None (default) = capture when the step is capturable; False = eager;
     True = capture or raise.  ``MULTIGRAD_GRAPH`` overrides None."""
 
     def __init__(self, model, comm=None, graph: Optional[bool] = None):
+        from ..models.onepoint import OnePointGroup
         self.model = model
-        self.comm = model.comm if comm is None else comm
+        self.group = isinstance(model, OnePointGroup)
+        self.members = tuple(model.models) if self.group else (model,)
+        default = model.main_comm if self.group else model.comm
+        self.comm = default if comm is None else comm
         self.size = 1 if self.comm is None else self.comm.size
         self.rank = 0 if self.comm is None else self.comm.rank
         env = os.environ.get("MULTIGRAD_GRAPH")
@@ -64,17 +119,56 @@ class GraphAdamEngine:
         self.graph = None
         self.use_graph = False
         self.fallback_reason = None
-        self.oneshot = None
+        self.oneshot = None          # main-communicator one-shot (group loss)
+        self.m_oneshot = [None] * len(self.members)  # per-member sumstat one-shot
         self.twoshot = None
         self.ar = None
-        self.mode = "adam"   # "sgd": fixed-rate gradient descent (run_simple_grad_descent)
+        self.mode = "adam"   # "sgd": fixed-rate gradient descent; "eval": scipy objective
+        self._gens = []
+        self._gen_i = 0
+        self._cap_key = _CaptureKey(self)
+        self.key_mode = None     # None | "step" | "const"
+        self.ready = False
+
+    # ------------------------------------------------------------------ keys
+    def _next_generator(self, device) -> torch.Generator:
+        dev = torch.device(device)
+        if dev.type != "cuda":
+            raise KeyNotCapturable(
+                f"randkey.generator({device!r}) inside a captured step: a host generator's "
+                f"draws would be frozen into the graph; use the model's CUDA device")
+        if dev.index is None:
+            dev = torch.device("cuda", torch.cuda.current_device())
+        if self._gen_i == len(self._gens):
+            self._gens.append(torch.Generator(device=dev))
+        g = self._gens[self._gen_i]
+        if g.device != dev:
+            raise KeyNotCapturable(f"randkey.generator({device!r}) on another device than "
+                                   f"the engine's {self.device}")
+        self._gen_i += 1
+        return g
+
+    def _step_key(self) -> Optional[PRNGKey]:
+        """This step's key (host; the eager driver's sequence, multigrad/adam.py:59-62)."""
+        if self.key_mode is None:
+            return None
+        if self.key_mode == "const":
+            return self.key
+        self.key, k = self.key.split(2)
+        return k
+
+    def _seed_generators(self, key: Optional[PRNGKey]) -> None:
+        if key is not None:
+            for g in self._gens:
+                g.manual_seed(key.seed)
 
     # ------------------------------------------------------------------ setup
     def setup(self, guess, nsteps: int, param_bounds=None, learning_rate: float = 0.01,
               b1: float = 0.9, b2: float = 0.999, eps: float = 1e-8, history="full",
-              legacy_bounds_jacobian: bool = False):
-        md = self.model
-        p0 = as_param_tensor(guess, device=md.param_device()).detach()
+              legacy_bounds_jacobian: bool = False, randkey=None, const_randkey: bool = False):
+        self.close()
+        md0 = self.members[0]
+        p0 = as_param_tensor(guess, device=md0.param_device()).detach()
         self.shape = tuple(p0.shape)
         p0 = p0.reshape(-1).to(torch.float32)
         dev = p0.device
@@ -83,34 +177,53 @@ class GraphAdamEngine:
         W = self.size
         self.lr, self.b1, self.b2, self.eps = float(learning_rate), float(b1), float(b2), float(eps)
         self.legacy = bool(legacy_bounds_jacobian)
+        if const_randkey:
+            assert randkey is not None, "Must pass randkey if const_randkey"
+            self.key_mode, self.key = "const", (randkey if hasattr(randkey, "split")
+                                                else init_randkey(randkey))
+        elif randkey is not None:
+            self.key_mode, self.key = "step", init_randkey(randkey)
+        else:
+            self.key_mode, self.key = None, None
         bounds = Bounds.from_spec(param_bounds, P, device=dev)
         cuda = dev.type == "cuda"
         sgd = self.mode in ("sgd", "eval")   # modes that need the summed gradient itself
         self.ar = None
-        if cuda and W > 1:
-            from ..parallel.xgmi import (connect_twoshot, get_oneshot, get_twoshot_allreduce,
+        self.twoshot = None
+        self.oneshot = None
+        self.m_oneshot = [None] * len(self.members)
+        if cuda:
+            from ..parallel.xgmi import (acquire_twoshot, get_oneshot, get_twoshot_allreduce,
                                          twoshot_enabled)
-            q = 4 * W
-            P_pad = -(-P // q) * q
-            if sgd:  # the summed gradient itself is needed: a capturable all-reduce
-                self.ar = get_twoshot_allreduce(self.comm, P)
-            else:
-                self.twoshot = connect_twoshot(self.comm, P_pad) if twoshot_enabled() else None
-            self.oneshot = get_oneshot(self.comm)
-        else:
-            P_pad = P
+            if W > 1:
+                q = 4 * W
+                P_pad = -(-P // q) * q
+                if sgd:  # the summed gradient itself is needed: a capturable all-reduce
+                    self.ar = get_twoshot_allreduce(self.comm, P)
+                else:
+                    self.twoshot = acquire_twoshot(self.comm, P_pad) if twoshot_enabled() else None
+                if self.group:
+                    self.oneshot = get_oneshot(self.comm)  # the group loss
+            # collective per sub-communicator (every member rank runs setup)
+            self.m_oneshot = [get_oneshot(md.comm) if md.comm is not None and md.comm.size > 1
+                              else None for md in self.members]
         self.P_pad = P_pad if self.twoshot is not None else P
         f32 = dict(dtype=torch.float32, device=dev)
+        # the hooks read p (cached memory); with the two-shot exchange the parameters live
+        # in its uncached peer-memory region and p is refreshed from it after each step
+        self.p = torch.zeros(self.P_pad, **f32)
         if self.twoshot is not None:
-            self.p = self.twoshot.theta
-            self.p.zero_()
+            self.theta = self.twoshot.theta
+            self.theta.zero_()
             self.gbuf = self.twoshot.grad
             self.gbuf.zero_()
         else:
-            self.p = torch.zeros(self.P_pad, **f32)
+            self.theta = self.p
             self.gbuf = None
         start = bounds.inverse(bounds.forward(p0)) if bounds is not None else p0
-        self.p[:P].copy_(start)
+        self.theta[:P].copy_(start)
+        if self.theta is not self.p:
+            self.p[:P].copy_(start)
         if bounds is not None and self.P_pad > P:
             pad = self.P_pad - P
             bounds = Bounds(torch.cat([bounds.lo, torch.full((pad,), -math.inf, **f32)]),
@@ -125,7 +238,7 @@ class GraphAdamEngine:
             self.bounds_loc = None if bounds is None else Bounds(
                 bounds.lo[lo_:lo_ + n_].contiguous(), bounds.hi[lo_:lo_ + n_].contiguous(),
                 bounds.kind[lo_:lo_ + n_].contiguous())
-            self.u = None if bounds is None else self.bounds_loc.forward(self.p[lo_:lo_ + n_]).contiguous()
+            self.u = None if bounds is None else self.bounds_loc.forward(self.theta[lo_:lo_ + n_]).contiguous()
         else:
             self.own = (0, self.P_pad)
             self.m = torch.zeros(self.P_pad, **f32)
@@ -140,7 +253,7 @@ class GraphAdamEngine:
         if self.twoshot is not None and history == "full":
             a, b = self.own
             self.traj_loc = torch.zeros((self.nsteps + 1, b - a), **f32)
-            self.traj_loc[0] = self.p[a:b]
+            self.traj_loc[0] = self.theta[a:b]
             self.history = History("last", nsteps, self.p[:P].clone())
         else:
             self.traj_loc = None
@@ -153,14 +266,19 @@ class GraphAdamEngine:
         self.graph = None
         self.tuning = None
         self._times = {}
+        self.fallback_reason = None
         exch = self.ar if sgd else self.twoshot
-        capturable = cuda and (W == 1 or (exch is not None and self.oneshot is not None))
+        capturable = cuda and (W == 1 or exch is not None) and \
+            (not self.group or W == 1 or self.oneshot is not None) and \
+            all(o is not None or md.comm is None or md.comm.size == 1
+                for o, md in zip(self.m_oneshot, self.members))
         if self.graph_req is True and not capturable:
             raise RuntimeError("this step is not capturable (RCCL collectives in it)")
         self.use_graph = capturable and self.graph_req is not False
-        if self.use_graph and W > 1 and not self._probe_capture():
-            # a rank's user hooks cannot be captured: every rank runs eagerly (a per-rank
-            # fallback would leave the ranks' collective sequences out of step)
+        if self.use_graph and not self._probe_capture(capture=W > 1):
+            # a rank's hooks cannot be captured, or a sumstat vector does not fit the
+            # one-shot kernel: every rank runs eagerly (a per-rank fallback would leave the
+            # ranks' collective sequences out of step)
             if self.graph_req is True:
                 raise RuntimeError(f"the step is not capturable: {self.fallback_reason}")
             self.use_graph = False
@@ -175,71 +293,135 @@ class GraphAdamEngine:
         self.ready = True
         return self
 
-    # ------------------------------------------------------------------ the step
-    def _hooks_only(self):
-        """The user's part of a step (forward, loss, cotangent, VJP) without collectives."""
-        md, P = self.model, self.P
-        with torch.enable_grad():
-            leaf = self.p[:P].detach().view(self.shape).requires_grad_(True)
-            partial = torch.as_tensor(md.calc_partial_sumstats_from_params(leaf))
-            total = partial.detach().clone().requires_grad_(True)
-            out = md.calc_loss_from_sumstats(total)
-            loss = out[0] if md.loss_func_has_aux else out
-            (cot,) = torch.autograd.grad(loss, total, allow_unused=True)
-            if cot is not None:
-                torch.autograd.grad(partial, leaf, cot, allow_unused=True)
+    def close(self) -> None:
+        """Give the two-shot context back to the communicator's pool (collective: every
+        rank closes its engine the same way); setup() calls it before re-connecting."""
+        if self.twoshot is not None:
+            from ..parallel.xgmi import release_twoshot
+            release_twoshot(self.comm, self.twoshot)
+        self.twoshot = None
+        self.ready = False
 
-    def _probe_capture(self) -> bool:
-        """Collective: can every rank capture its user hooks?  Each rank captures the
-        collective-free part of a step into a throw-away graph; the verdicts are all-gathered
+    # ------------------------------------------------------------------ the step
+    def _member(self, i: int, key, exchange: bool):
+        """Member i's chain rule up to its local VJP: ``(loss, g_local)``; with
+        ``exchange`` the partial sumstats are summed over the member's communicator."""
+        md, P = self.members[i], self.P
+        rk = {} if key is None else {"randkey": key}
+        with torch.enable_grad():
+            leaf = _leaf_view(self.p[:P], self.shape)
+            out = md.calc_partial_sumstats_from_params(leaf, **rk)
+            if md.sumstats_func_has_aux:
+                partial, saux = out
+            else:
+                partial, saux = out, None
+            partial = torch.as_tensor(partial)
+            self._S_meta[i] = (partial.dtype, partial.numel())
+            total = partial.detach().clone()
+            if exchange:
+                total = self._sumstats_allreduce(i, total)
+            total = total.to(partial.dtype).requires_grad_(True)
+            args = (total, saux) if md.sumstats_func_has_aux else (total,)
+            lout = md.calc_loss_from_sumstats(*args, **rk)
+            loss = lout[0] if md.loss_func_has_aux else lout
+            (cot,) = torch.autograd.grad(loss, total, allow_unused=True)
+            if cot is None:
+                cot = torch.zeros_like(total)
+            g = None
+            if partial.requires_grad:
+                (g,) = torch.autograd.grad(partial, leaf, cot, allow_unused=True)
+        return loss.detach(), g
+
+    def _hooks_only(self, key):
+        """The user's part of a step (forward, loss, cotangent, VJP) without collectives."""
+        self._S_meta = [None] * len(self.members)
+        self._gen_i = 0
+        for i in range(len(self.members)):
+            self._member(i, key, exchange=False)
+
+    def _probe_capture(self, capture: bool) -> bool:
+        """Collective on several ranks: can every rank capture its user hooks?  The
+        collective-free part of a step runs once eagerly on a side stream (lazy
+        initialisation; it also records the sumstat shapes and counts the randkey
+        generators) and, with ``capture``, into a throw-away graph; every sumstat vector
+        summed over more than one rank must fit the one-shot kernel (fp32, <= 64 values:
+        an RCCL call must never be recorded into a graph).  The verdicts are all-gathered
         so all ranks take the same path."""
+        from ..parallel.xgmi import MAX_FLOATS
         ok, reason = True, None
+        key = self._cap_key if self.key_mode is not None else None
         try:
             s = torch.cuda.Stream()
             s.wait_stream(torch.cuda.current_stream())
             with torch.cuda.stream(s):
-                self._hooks_only()   # lazy initialisation outside the capture
+                self._hooks_only(key)
             torch.cuda.current_stream().wait_stream(s)
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                self._hooks_only()
-            del g
+            for i, md in enumerate(self.members):
+                if md.comm is not None and md.comm.size > 1:
+                    dt, n = self._S_meta[i]
+                    if dt != torch.float32 or n > MAX_FLOATS:
+                        raise RuntimeError(
+                            f"sumstats of {n} x {dt} do not fit the capturable one-shot "
+                            f"all-reduce (fp32, <= {MAX_FLOATS} values)")
+            if capture:
+                g = torch.cuda.CUDAGraph()
+                for gen in self._gens:
+                    g.register_generator_state(gen)
+                with torch.cuda.graph(g):
+                    self._hooks_only(key)
+                del g
         except Exception as exc:  # noqa: BLE001  (host sync / dynamic shapes in user code)
             torch.cuda.synchronize()
             ok, reason = False, f"capture failed: {type(exc).__name__}: {exc}"
-        verdicts = self.comm.allgather((ok, reason))
+        if self.size > 1:
+            verdicts = self.comm.allgather((ok, reason))
+        else:
+            verdicts = [(ok, reason)]
         bad = [(r, why) for r, (good, why) in enumerate(verdicts) if not good]
         if bad:
-            self.fallback_reason = f"rank {bad[0][0]}: {bad[0][1]}"
+            self.fallback_reason = f"rank {bad[0][0]}: {bad[0][1]}" if self.size > 1 else bad[0][1]
         return not bad
 
-    def _sumstats_allreduce(self, S: torch.Tensor) -> torch.Tensor:
-        self._nS = S.numel()
-        if self.size == 1:
+    def _sumstats_allreduce(self, i: int, S: torch.Tensor) -> torch.Tensor:
+        mc = self.members[i].comm
+        if mc is None or mc.size == 1:
             return S
         S = S.contiguous()
-        if self.oneshot is not None and S.dtype == torch.float32 and S.numel() <= 64:
-            self.oneshot(S)
+        o = self.m_oneshot[i]
+        if o is not None and S.dtype == torch.float32 and S.numel() <= 64:
+            o(S)
             return S
-        self.comm.all_reduce(S)
+        mc.all_reduce(S)
         return S
 
-    def _body(self, host_step: Optional[int]):
-        md, P = self.model, self.P
-        with torch.enable_grad():
-            leaf = self.p[:P].detach().view(self.shape).requires_grad_(True)
-            partial = torch.as_tensor(md.calc_partial_sumstats_from_params(leaf))
-            if md.sumstats_func_has_aux:
-                raise TypeError("the graph engine needs sumstats without aux")
-            total = self._sumstats_allreduce(partial.detach().clone())
-            total = total.to(partial.dtype).requires_grad_(True)
-            out = md.calc_loss_from_sumstats(total)
-            loss = out[0] if md.loss_func_has_aux else out
-            (cot,) = torch.autograd.grad(loss, total, allow_unused=True)
-            if cot is None:
-                cot = torch.zeros_like(total)
-            (g,) = torch.autograd.grad(partial, leaf, cot, allow_unused=True)
-        self.loss.copy_(loss.detach().reshape(1).to(torch.float32))
+    def _group_loss(self, losses) -> torch.Tensor:
+        """Sum of the members' losses over the group: sub-communicator rank 0 contributes."""
+        tot = torch.zeros(1, dtype=torch.float32, device=self.device)
+        for md, l in zip(self.members, losses):
+            if md.comm is None or md.comm.rank == 0:
+                tot = tot + l.reshape(1).to(torch.float32)
+        if self.size > 1:
+            tot = tot.contiguous()
+            if self.oneshot is not None:
+                self.oneshot(tot)
+            else:
+                self.comm.all_reduce(tot)
+        return tot
+
+    def _body(self, host_step: Optional[int], key):
+        P = self.P
+        self._S_meta = [None] * len(self.members)
+        self._gen_i = 0
+        g, losses = None, []
+        for i in range(len(self.members)):
+            loss, gi = self._member(i, key, exchange=True)
+            losses.append(loss)
+            if gi is not None:
+                g = gi if g is None else g + gi
+        if self.group:
+            self.loss.copy_(self._group_loss(losses))
+        else:
+            self.loss.copy_(losses[0].reshape(1).to(torch.float32))
         g = torch.zeros(self.shape, device=self.device) if g is None else g
         g = g.reshape(-1).to(torch.float32)
         if self.mode == "eval":
@@ -278,6 +460,7 @@ class GraphAdamEngine:
                               traj=traj, traj_stride=0 if traj is None else b - a,
                               step=self.step_dev, host_step=host_step, lr=self.lr, b1=self.b1,
                               b2=self.b2, eps=self.eps)
+            self.p[:P].copy_(self.theta[:P])  # the cached copy the next step's hooks read
             return
         if self.size > 1:
             g = g.contiguous()
@@ -292,16 +475,20 @@ class GraphAdamEngine:
         state the warm-up moved, then capture one step.  Collectives in the warm-up run on
         every rank alike, so their device sequence numbers stay in lockstep."""
         saved = [t.clone() for t in (self.p, self.m, self.v, self.step_dev)]
+        th_saved = self.theta.clone() if self.theta is not self.p else None
         u_saved = self.u.clone() if self.u is not None and self.u is not self.p else None
         traj_saved = None if self.traj_loc is None else self.traj_loc[1].clone()
         hist_saved = None if self.history.mode != "full" else self.history.buf[1].clone()
+        key = self._cap_key if self.key_mode is not None else None
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
-            self._body(None)  # one warm-up step (it writes trajectory row 1, restored below)
+            self._body(None, key)  # one warm-up step (it writes trajectory row 1, restored below)
         torch.cuda.current_stream().wait_stream(s)
         for t, v in zip((self.p, self.m, self.v, self.step_dev), saved):
             t.copy_(v)
+        if th_saved is not None:
+            self.theta.copy_(th_saved)
         if u_saved is not None:
             self.u.copy_(u_saved)
         if traj_saved is not None:
@@ -309,13 +496,19 @@ class GraphAdamEngine:
         if hist_saved is not None:
             self.history.buf[1].copy_(hist_saved)
         graph = torch.cuda.CUDAGraph()
+        for gen in self._gens:
+            graph.register_generator_state(gen)
         with torch.cuda.graph(graph):
-            self._body(None)
+            self._body(None, key)
         return graph
+
+    def _replay(self, key) -> None:
+        self._seed_generators(key)
+        self.graph.replay()
 
     _TUNE = 3  # steps timed per mode by the auto policy
 
-    def _tuned_step(self):
+    def _tuned_step(self, key):
         """Auto policy (``graph=None``): the first steps run eagerly, the next ones from
         the captured graph; each window of steps is timed as a whole (no synchronisation
         inside it, so eager launches overlap the GPU as in steady state) and the faster
@@ -335,15 +528,15 @@ class GraphAdamEngine:
                 torch.cuda.synchronize()
                 self.use_graph = False
                 self.fallback_reason = f"capture failed: {type(exc).__name__}: {exc}"
-                self._body(k)
+                self._body(k, key)
                 return
         if k in (0, T):
             torch.cuda.synchronize()
             self._t0 = time.perf_counter()
         if mode == "graph":
-            self.graph.replay()
+            self._replay(key)
         else:
-            self._body(k)
+            self._body(k, key)
         if k in (T - 1, 2 * T - 1):
             torch.cuda.synchronize()
             self._times[mode] = time.perf_counter() - self._t0
@@ -363,9 +556,10 @@ class GraphAdamEngine:
         if self.step_host >= self.nsteps and (self.history.mode == "full" or self.traj_loc is not None
                                               or self.mode == "sgd"):
             raise RuntimeError("more steps than the trajectory buffer was sized for")
+        key = self._step_key()
         if self.use_graph and self.graph_req is None and self.tuning is None and \
                 self.nsteps > 2 * self._TUNE:
-            self._tuned_step()
+            self._tuned_step(key)
             self.step_host += 1
             if self.history.mode != "full" and self.traj_loc is None:
                 self.history.record(self.step_host - 1, self.p[:self.P])
@@ -380,9 +574,9 @@ class GraphAdamEngine:
                 self.use_graph = False
                 self.fallback_reason = f"capture failed: {type(exc).__name__}: {exc}"
         if self.use_graph:
-            self.graph.replay()
+            self._replay(key)
         else:
-            self._body(self.step_host)
+            self._body(self.step_host, key)
         self.step_host += 1
         if self.history.mode != "full" and self.traj_loc is None:
             self.history.record(self.step_host - 1, self.p[:self.P])
@@ -393,6 +587,10 @@ class GraphAdamEngine:
         for ctx in (self.twoshot, self.ar, self.oneshot):
             if ctx is not None:
                 ctx.check(where or f"generic engine step {self.step_host}", comm=comm)
+        for md, ctx in zip(self.members, self.m_oneshot):
+            if ctx is not None:
+                ctx.check(where or f"generic engine step {self.step_host}",
+                          comm=md.comm if collective else None)
 
     def last_loss(self) -> float:
         v = float(self.loss.item())
@@ -416,14 +614,16 @@ class GraphAdamEngine:
         t = self.history.result()[:, :self.P] if self.history.mode == "full" else self.history.result()
         return t.reshape((t.shape[0],) + self.shape)
 
-    def evaluator(self, x0):
+    def evaluator(self, x0, randkey=None):
         """``f(x) -> (loss, grad)`` replaying one captured evaluation of the distributed
         chain rule (autograd forward, sumstat all-reduce, cotangent, VJP, gradient sum):
         the objective of the root-driven scipy L-BFGS-B (optim/bfgs.py), which calls it
-        once per function evaluation.  Falls back to eager launches when the step cannot
-        be captured; collective on several ranks (every rank evaluates every point)."""
+        once per function evaluation with a constant ``randkey`` (multigrad/bfgs.py:63-66).
+        Falls back to eager launches when the step cannot be captured; collective on
+        several ranks (every rank evaluates every point)."""
         self.mode = "eval"
-        self.setup(x0, nsteps=1, history="last")
+        self.setup(x0, nsteps=1, history="last", randkey=randkey,
+                   const_randkey=randkey is not None)
         P, shape = self.P, self.shape
         if self.use_graph and self.graph_req is not False:
             try:
@@ -436,13 +636,15 @@ class GraphAdamEngine:
                 self.fallback_reason = f"capture failed: {type(exc).__name__}: {exc}"
 
         def f(x, **kw):
+            kw.pop("randkey", None)  # the engine holds the (constant) key
             if kw:
                 raise TypeError(f"the captured evaluator takes no keywords: {sorted(kw)}")
             self.p[:P].copy_(torch.as_tensor(x).reshape(-1))
+            key = self._step_key()
             if self.use_graph:
-                self.graph.replay()
+                self._replay(key)
             else:
-                self._body(None)
+                self._body(None, key)
             out = self.lg.cpu()  # loss and gradient in ONE device->host copy
             return out[0], out[1:].reshape(shape)
 
@@ -465,30 +667,35 @@ class GraphAdamEngine:
                     hooks(i, self.loss, None, self.params)
         self.check("simple_grad_descent", collective=True)
         n = self.step_host
-        return GradDescentResult(loss=self.loss_hist[:n].clone(),
-                                 params=self.param_hist[:n].reshape((n,) + self.shape).clone(),
-                                 aux=[None] * n)
+        res = GradDescentResult(loss=self.loss_hist[:n].clone(),
+                                params=self.param_hist[:n].reshape((n,) + self.shape).clone(),
+                                aux=[None] * n)
+        self.close()
+        return res
 
     def run_adam(self, guess, nsteps: int = 100, param_bounds=None, learning_rate: float = 0.01,
                  b1: float = 0.9, b2: float = 0.999, eps: float = 1e-8, history="full",
-                 legacy_bounds_jacobian: bool = False, callback=None, **unused):
+                 legacy_bounds_jacobian: bool = False, callback=None, randkey=None,
+                 const_randkey: bool = False, **unused):
         """Adam with the reference's contract: trajectory ``(nsteps+1, *shape)``."""
         if unused:
             raise TypeError(f"unsupported run_adam options for the graph engine: {sorted(unused)}")
         from ..utils.hooks import StepHooks, driver_guard
         self.mode = "adam"
         self.setup(guess, nsteps, param_bounds, learning_rate, b1, b2, eps, history,
-                   legacy_bounds_jacobian)
+                   legacy_bounds_jacobian, randkey=randkey, const_randkey=const_randkey)
         hooks = StepHooks(self.comm, callback)
         with driver_guard(self.comm):
-            W = self.comm.size
+            W = self.size
 
             def comm_bytes():  # sumstat exchange + dense-gradient exchange, bytes sent
-                nS = getattr(self, "_nS", 0)
+                nS = sum(m[1] for m in getattr(self, "_S_meta", []) if m is not None)
                 return 0 if W == 1 else int(4 * (W - 1) * (nS + 2 * (self.P // W)))
 
             for i in range(int(nsteps)):
                 self.step()
                 if hooks.active:
                     hooks(i, self.loss, self, self.params, comm_bytes=comm_bytes)
-            return self.trajectory()
+            traj = self.trajectory()
+        self.close()
+        return traj

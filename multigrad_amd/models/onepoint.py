@@ -49,14 +49,20 @@ class _OptimizerFrontEnds:
     def param_device(self) -> torch.device:
         raise NotImplementedError
 
-    def _generic_engine_ok(self, x0) -> bool:
-        """Whether this model's GD / scipy-BFGS evaluations can go through the captured
-        generic engine: a single torch OnePointModel (not a group) on a GPU, fp32, no aux
-        outputs, without the fused-engine protocol, not disabled."""
-        return (isinstance(self, OnePointModel) and x0.is_cuda and x0.dtype == torch.float32
-                and not getattr(self, "loss_func_has_aux", False)
-                and not getattr(self, "sumstats_func_has_aux", False)
-                and getattr(self, "fused_engine", None) is None
+    def _engine_members(self):
+        return tuple(self.models) if isinstance(self, OnePointGroup) else (self,)
+
+    def _generic_engine_ok(self, x0, loss_aux_ok: bool = True) -> bool:
+        """Whether this model's (or group's) optimizer steps can go through the captured
+        generic engine (engine/generic.py): torch OnePointModels on a GPU, an fp32 guess
+        (the engine's Adam state is fp32; an fp64 fit keeps the eager loop), no fused-engine
+        protocol (a single model that has one uses the fused engine), not disabled."""
+        members = self._engine_members()
+        single_fused = (not isinstance(self, OnePointGroup)
+                        and getattr(self, "fused_engine", None) is not None)
+        return (x0.is_cuda and x0.dtype == torch.float32 and not single_fused
+                and all(isinstance(m, OnePointModel) for m in members)
+                and (loss_aux_ok or not any(m.loss_func_has_aux for m in members))
                 and os.environ.get("MULTIGRAD_GENERIC_ENGINE", "1") != "0")
 
     def run_simple_grad_descent(self, guess, nsteps: int = 100, learning_rate: float = 0.01):
@@ -67,7 +73,7 @@ class _OptimizerFrontEnds:
         """
         has_aux = bool(getattr(self, "loss_func_has_aux", False))
         x0 = as_param_tensor(guess, device=self.param_device())
-        if self._generic_engine_ok(x0):
+        if self._generic_engine_ok(x0, loss_aux_ok=False):
             # one captured step replayed per iteration (engine/generic.py)
             from ..engine.generic import GraphAdamEngine
             return GraphAdamEngine(self, comm=self._opt_comm()).run_simple_grad_descent(
@@ -102,22 +108,27 @@ class _OptimizerFrontEnds:
                 return self.calc_loss_and_grad_from_params(x, **k)
         fused = getattr(self, "fused_engine", None)
         use_engine = kw.pop("use_engine", True)
-        if fused is not None and randkey is None and not const_randkey and use_engine:
+        keyed = randkey is not None or const_randkey
+        if fused is not None and use_engine and (
+                not keyed or getattr(self, "engine_randkey_invariant", False)):
+            # a fused-protocol model whose hooks ignore randkey gives the same trajectory
+            # with or without keys (engine_randkey_invariant)
             eng = fused()
             if eng is not None:
-                return eng.run_adam(guess, nsteps=nsteps, param_bounds=param_bounds,
-                                    learning_rate=learning_rate, **kw)
-        # any other model on a GPU: one captured step replayed per iteration
-        # (engine/generic.py), unless per-step keys or unsupported options need the loop
+                try:
+                    return eng.run_adam(guess, nsteps=nsteps, param_bounds=param_bounds,
+                                        learning_rate=learning_rate, **kw)
+                finally:
+                    eng.close()
+        # any other model or group on a GPU: one captured step replayed per iteration
+        # (engine/generic.py), per-step or constant keys included
         graph_kw = {k: kw[k] for k in kw if k in ("history", "legacy_bounds_jacobian", "b1",
                                                    "b2", "eps", "callback")}
-        if fused is None and use_engine and randkey is None and not const_randkey and \
-                isinstance(self, OnePointModel) and len(graph_kw) == len(kw) and guess.is_cuda and \
-                not getattr(self, "sumstats_func_has_aux", False) and \
-                os.environ.get("MULTIGRAD_GENERIC_ENGINE", "1") != "0":
+        if use_engine and len(graph_kw) == len(kw) and self._generic_engine_ok(guess):
             from ..engine.generic import GraphAdamEngine
             return GraphAdamEngine(self, comm=comm).run_adam(
                 guess, nsteps=nsteps, param_bounds=param_bounds, learning_rate=learning_rate,
+                randkey=const_key if const_randkey else randkey, const_randkey=const_randkey,
                 **graph_kw)
         return _adam.run_adam(loss_and_grad_fn, params=guess, data=None, nsteps=nsteps,
                               param_bounds=param_bounds, learning_rate=learning_rate,
@@ -142,13 +153,20 @@ class _OptimizerFrontEnds:
             method = "device" if x0.numel() > 100_000 else "scipy"
         if method == "scipy":
             fn = self.calc_loss_and_grad_from_params
-            if randkey is None and self._generic_engine_ok(x0):
+            eng = None
+            if self._generic_engine_ok(x0):
                 # each scipy evaluation replays one captured evaluation (engine/generic.py)
                 from ..engine.generic import GraphAdamEngine
-                fn = GraphAdamEngine(self, comm=comm).evaluator(x0)
-            return _bfgs.run_bfgs(fn, x0, maxsteps=maxsteps,
-                                  param_bounds=param_bounds, randkey=randkey, comm=comm,
-                                  device=self.param_device(), **kw)
+                eng = GraphAdamEngine(self, comm=comm)
+                fn = eng.evaluator(x0, randkey=None if randkey is None else init_randkey(randkey)
+                                   if not hasattr(randkey, "split") else randkey)
+            try:
+                return _bfgs.run_bfgs(fn, x0, maxsteps=maxsteps,
+                                      param_bounds=param_bounds, randkey=randkey, comm=comm,
+                                      device=self.param_device(), **kw)
+            finally:
+                if eng is not None:
+                    eng.close()
         from ..optim import lbfgs as _lbfgs
         from ..optim import lbfgsb as _lbfgsb
         hist = kw.pop("history", 10)
@@ -159,11 +177,14 @@ class _OptimizerFrontEnds:
         if fused is not None and randkey is None and (param_bounds is None or mode == "project"):
             eng = fused(comm=comm, **{k: kw.pop(k) for k in ("zero", "chunks") if k in kw})
             if eng is not None:
-                obj = eng.lbfgs_objective(x0)
-                if param_bounds is None:
-                    return _lbfgs.lbfgs_minimize(obj, maxiter=maxsteps, m=hist, **kw)
-                lo, hi = obj.local_box(param_bounds)
-                return _lbfgsb.lbfgsb_minimize(obj, lo, hi, maxiter=maxsteps, m=hist, **kw)
+                try:
+                    obj = eng.lbfgs_objective(x0)
+                    if param_bounds is None:
+                        return _lbfgs.lbfgs_minimize(obj, maxiter=maxsteps, m=hist, **kw)
+                    lo, hi = obj.local_box(param_bounds)
+                    return _lbfgsb.lbfgsb_minimize(obj, lo, hi, maxiter=maxsteps, m=hist, **kw)
+                finally:
+                    eng.close()
         if param_bounds is not None and mode == "project":
             return _lbfgsb.run_lbfgsb_device(self.calc_loss_and_grad_from_params, x0,
                                              maxsteps=maxsteps, param_bounds=param_bounds,

@@ -183,6 +183,10 @@ class PopulationSMFModel(OnePointModel):
 
     aux_data: dict = None
 
+    # the hooks ignore randkey (a deterministic model), so a keyed run_adam gives the
+    # keyless trajectory and may use the fused engine
+    engine_randkey_invariant = True
+
     @property
     def shard(self) -> PopulationShard:
         return self.aux_data["shard"]

@@ -17,7 +17,7 @@ import torch
 from ..ops.smf import logmse_loss
 from .onepoint import OnePointModel
 
-__all__ = ["TorchPopulationSMFModel", "torch_population_data"]
+__all__ = ["TorchPopulationSMFModel", "StochasticTorchPopulationSMFModel", "torch_population_data"]
 
 
 def torch_population_data(data: dict) -> dict:
@@ -42,14 +42,34 @@ class TorchPopulationSMFModel(OnePointModel):
     aux_data: dict = None
 
     def calc_partial_sumstats_from_params(self, params, randkey=None):
+        return self._sumstats(params, self.aux_data["x"])
+
+    def _sumstats(self, params, x):
         d = self.aux_data
         th = params.reshape(-1, 2)
         a = th[:, 0][d["pop"]]
         sigma = torch.pow(10.0, th[:, 1])[d["pop"]]
-        z = (d["edges"][None, :] - (d["x"] + a)[:, None]) / sigma[:, None]
+        z = (d["edges"][None, :] - (x + a)[:, None]) / sigma[:, None]
         cdf = torch.special.ndtr(z)
         return (cdf[:, 1:] - cdf[:, :-1]).sum(0) * d["scale"]
 
     def calc_loss_from_sumstats(self, sumstats, sumstats_aux=None, randkey=None):
         d = self.aux_data
         return logmse_loss(sumstats, d["target"].to(sumstats.dtype), d["eps"])
+
+
+@dataclass(eq=False)
+class StochasticTorchPopulationSMFModel(TorchPopulationSMFModel):
+    """The same model with per-evaluation Monte-Carlo scatter: every halo's log mass is
+    perturbed by ``scatter * N(0, 1)`` drawn from ``randkey.generator(device)`` -- a
+    stochastic forward model, fitted with a fresh key per Adam step (reference
+    multigrad/adam.py:59-62) or a constant one (``const_randkey``)."""
+
+    scatter: float = 0.02
+
+    def calc_partial_sumstats_from_params(self, params, randkey=None):
+        x = self.aux_data["x"]
+        if randkey is not None:
+            x = x + self.scatter * torch.randn(x.shape, generator=randkey.generator(x.device),
+                                               device=x.device, dtype=x.dtype)
+        return self._sumstats(params, x)

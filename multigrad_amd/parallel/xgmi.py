@@ -35,10 +35,37 @@ import torch
 
 __all__ = ["OneShotAllReduce", "CollectiveTimeout", "oneshot_enabled", "oneshot_mode",
            "connect", "get_oneshot", "maybe_oneshot", "MAX_FLOATS", "MAX_RANKS", "TwoShot",
-           "connect_twoshot", "twoshot_enabled", "get_twoshot_allreduce"]
+           "connect_twoshot", "twoshot_enabled", "get_twoshot_allreduce", "acquire_twoshot",
+           "release_twoshot", "status", "STRESS_REPS"]
 
 MAX_FLOATS = 64
 MAX_RANKS = 8
+STRESS_REPS = 32   # back-to-back device-only exchanges in each connect-time self-test
+
+
+def _corrupt_rank() -> int:
+    """Test hook: the rank that corrupts one self-test exchange (-1: none)."""
+    try:
+        return int(os.environ.get("MULTIGRAD_XGMI_SELFTEST_CORRUPT", "-1"))
+    except ValueError:
+        return -1
+
+
+def _record(comm, kind: str, **info) -> None:
+    """Per-communicator verdict log of the peer-memory contexts (``status(comm)``)."""
+    try:
+        log = comm.__dict__.setdefault("_xgmi_status", {})
+    except AttributeError:
+        return
+    log.setdefault(kind, []).append(info)
+
+
+def status(comm) -> dict:
+    """What the connect-time checks of ``comm``'s peer-memory collectives decided:
+    ``{"one-shot": [...], "two-shot": [...]}``, one entry per connect attempt with
+    ``ok``, the number of stress exchanges that passed and the fallback reason (RCCL)
+    otherwise.  bench.py records it in its JSON line."""
+    return dict(getattr(comm, "_xgmi_status", {}) or {})
 
 
 class CollectiveTimeout(RuntimeError):
@@ -121,17 +148,33 @@ class OneShotAllReduce:
         torch.cuda.synchronize()
         comm.barrier()
 
-    def self_test(self) -> bool:
-        """A few calls with rank-dependent values whose sums are exact in fp32; True when
-        every result is right and no wait timed out."""
+    def self_test(self, reps: int = STRESS_REPS) -> bool:
+        """Stress self-test on the real peers: ``reps`` back-to-back exchanges with no host
+        synchronisation in between, each with step-unique rank-dependent values whose sums
+        are exact in fp32 (so a read of the previous exchange's slot, a lost flag or a
+        reordered store shows up as a wrong sum), every result copied aside on the device
+        and verified once at the end.  True when every sum is right and no wait timed
+        out.  ``MULTIGRAD_XGMI_SELFTEST_CORRUPT=<rank>`` (test hook) makes that rank
+        perturb its contribution to one exchange, so every rank must fail."""
         dev = self.seq.device
-        for i in range(8):
-            n = 1 + (7 * i) % MAX_FLOATS
-            t = torch.arange(n, device=dev, dtype=torch.float32) + (self.rank + 1) * (i + 1)
+        corrupt = _corrupt_rank() == self.rank
+        res = torch.zeros((reps, MAX_FLOATS), dtype=torch.float32, device=dev)
+        bufs = [torch.empty(1 + (7 * i) % MAX_FLOATS, dtype=torch.float32, device=dev)
+                for i in range(reps)]
+        for i, t in enumerate(bufs):
+            n = t.numel()
+            torch.arange(n, out=t)
+            t.add_((self.rank + 1) * (i + 1))
+            if corrupt and i == reps // 2:
+                t.add_(0.5)
             self(t)
+            res[i, :n].copy_(t)
+        got = res.cpu()
+        for i, t in enumerate(bufs):
+            n = t.numel()
             want = (torch.arange(n, dtype=torch.float32) * self.size
                     + (i + 1) * self.size * (self.size + 1) / 2)
-            if not torch.equal(t.cpu(), want):
+            if not torch.equal(got[i, :n], want):
                 return False
         return self.ok()
 
@@ -175,14 +218,21 @@ def connect(comm, timeout_s: float = 5.0, test: bool = True) -> Optional[OneShot
                     E.xgmi_close(p)
             if base:
                 E.xgmi_free(base)
+        _record(comm, "one-shot", ok=False, stress_exchanges=0,
+                fallback="RCCL: peer-memory export/map unavailable on some rank")
         return None
     ar = OneShotAllReduce(comm.rank, comm.size, base, peers, timeout_s)
     comm.barrier()  # every region is zeroed and mapped before any rank writes into it
     ok = ar.self_test() if test else True
-    if not all(comm.allgather(bool(ok))):
+    verdicts = comm.allgather(bool(ok))
+    if not all(verdicts):
         torch.cuda.synchronize()
         ar.close()
+        _record(comm, "one-shot", ok=False, stress_exchanges=0,
+                fallback=f"RCCL: stress self-test failed on rank(s) "
+                         f"{[r for r, v in enumerate(verdicts) if not v]}")
         return None
+    _record(comm, "one-shot", ok=True, stress_exchanges=STRESS_REPS if test else 0, fallback=None)
     return ar
 
 
@@ -310,25 +360,42 @@ class TwoShot:
     def ok(self) -> bool:
         return int(self.err.item()) == 0
 
-    def self_test(self) -> bool:
-        """Two exchanges (mode 0) of rank-dependent gradients whose sums are exact in fp32:
-        every rank's ``theta`` must hold the full sum afterwards."""
+    def self_test(self, reps: int = STRESS_REPS) -> bool:
+        """Stress self-test: ``reps`` back-to-back mode-0 exchanges over the whole region
+        with no host synchronisation in between.  Exchange i sums gradients
+        ``(idx mod 97) + (rank + 1)(i + 1)`` -- exact in fp32 and different in every
+        exchange, so a slice pulled from a peer before it was rewritten (the previous
+        exchange's value), a parameter slice that did not land, or a flag raised too early
+        all give a wrong sum.  A strided sample of ``theta`` covering every rank's slice is
+        copied aside on the device after each exchange and verified once at the end.
+        ``MULTIGRAD_XGMI_SELFTEST_CORRUPT=<rank>`` (test hook): that rank corrupts its
+        gradient slice in one exchange, so every rank must fail."""
         dev = self.grad.device
+        corrupt = _corrupt_rank() == self.rank
+        stride = max(1, self.numel // 4096)
+        sample = torch.arange(0, self.numel, stride, device=dev)
         idx = torch.arange(self.numel, device=dev, dtype=torch.float32)
-        for rep in range(2):
-            self.grad.copy_(torch.remainder(idx, 97.0) + (self.rank + 1) * (rep + 1))
-            torch.cuda.synchronize()
-            lo, n = self.slice()
+        base = torch.remainder(idx, 97.0)
+        res = torch.empty((reps, sample.numel()), dtype=torch.float32, device=dev)
+        lo, n = self.slice()
+        for i in range(reps):
+            torch.add(base, float((self.rank + 1) * (i + 1)), out=self.grad)
+            if corrupt and i == reps // 2:
+                self.grad[::7].add_(0.5)
             self.step(lo, n, 0)
-            torch.cuda.synchronize()
-            want = (torch.remainder(idx, 97.0) * self.size
-                    + (rep + 1) * self.size * (self.size + 1) / 2)
-            if not torch.equal(self.theta, want):
-                return False
+            res[i].copy_(self.theta[sample])
+        got = res.cpu()
+        b = base[sample].cpu()
+        ok = True
+        for i in range(reps):
+            want = b * self.size + (i + 1) * self.size * (self.size + 1) / 2
+            if not torch.equal(got[i], want):
+                ok = False
+                break
         self.grad.zero_()
         self.theta.zero_()
         torch.cuda.synchronize()
-        return self.ok()
+        return ok and self.ok()
 
     def reset(self, comm) -> None:
         from ..ops._ext import ext
@@ -356,11 +423,20 @@ class TwoShot:
         self.grad = self.theta = None
 
 
+_MAX_AR_CONTEXTS = 4
+
+
 def get_twoshot_allreduce(comm, numel: int) -> Optional[TwoShot]:
     """A cached two-shot context able to sum ``numel`` fp32 values over ``comm`` (for
     capturable user-level all-reduces, :func:`multigrad_amd.ingraph.reduce_sum`);
     collective on first use for a given size class.  None when disabled or unavailable
-    (the caller uses RCCL)."""
+    (the caller uses RCCL).
+
+    The smallest cached context that is large enough is reused.  Connecting is
+    collective and synchronises the host, so it is refused while a graph is being
+    captured (connect before capturing: call once eagerly with the same size).  At most
+    ``_MAX_AR_CONTEXTS`` working contexts are kept; connecting a larger one closes the
+    smallest (every rank makes the same calls in the same order, so the caches agree)."""
     if (comm is None or comm.size < 2 or comm.size > MAX_RANKS or not twoshot_enabled()
             or not torch.cuda.is_available()):
         return None
@@ -369,12 +445,55 @@ def get_twoshot_allreduce(comm, numel: int) -> Optional[TwoShot]:
     cache = getattr(comm, "_twoshot_ar", None)
     if cache is None:
         cache = comm._twoshot_ar = {}
-    for have, ts in cache.items():
-        if have >= want:
-            return ts or None
+    fits = sorted(have for have, ts in cache.items() if ts and have >= want)
+    if fits:
+        return cache[fits[0]]
+    if any(not ts and have <= want for have, ts in cache.items()):
+        return None  # a failed connect at this size or below: the peers are unusable
+    if torch.cuda.is_current_stream_capturing():
+        raise RuntimeError(
+            f"two-shot all-reduce of {numel} floats: no connected context is large enough "
+            f"and connecting is collective (host synchronisation), which a graph capture "
+            f"cannot contain; run one eager call of this size on every rank first")
     ts = connect_twoshot(comm, want, _timeout_s()) or False
     cache[want] = ts
+    live = sorted(have for have, t in cache.items() if t)
+    while len(live) > _MAX_AR_CONTEXTS:
+        torch.cuda.synchronize()
+        comm.barrier()
+        cache.pop(live[0]).close()
+        live.pop(0)
     return ts or None
+
+
+def acquire_twoshot(comm, numel: int) -> Optional[TwoShot]:
+    """Collective: a two-shot context of exactly ``numel`` floats for an engine, taken
+    from ``comm``'s pool of released contexts when every rank has one (no new peer
+    memory, no new IPC mappings), connected (and stress-tested) otherwise.  Give it back
+    with :func:`release_twoshot` when the engine is done."""
+    pool = comm.__dict__.setdefault("_twoshot_pool", {})
+    free = pool.get(int(numel), [])
+    if all(comm.allgather(bool(free))):
+        ts = free.pop()
+        torch.cuda.synchronize()
+        ts.theta.zero_()
+        ts.grad.zero_()
+        return ts
+    return connect_twoshot(comm, numel)
+
+
+def release_twoshot(comm, ts: Optional[TwoShot], keep: int = 2) -> None:
+    """Return an engine's two-shot context to ``comm``'s pool (``keep`` per size; the
+    rest are closed).  Every rank releases in the same order, so the pools stay paired."""
+    if ts is None or not ts.regions:
+        return
+    torch.cuda.synchronize()
+    pool = comm.__dict__.setdefault("_twoshot_pool", {})
+    free = pool.setdefault(ts.numel, [])
+    free.append(ts)
+    while len(free) > keep:
+        comm.barrier()
+        free.pop(0).close()
 
 
 def connect_twoshot(comm, numel: int, timeout_s: Optional[float] = None,
@@ -416,11 +535,19 @@ def connect_twoshot(comm, numel: int, timeout_s: Optional[float] = None,
                         E.xgmi_close(p)
             for b in regions:
                 E.xgmi_free(b)
+        _record(comm, "two-shot", ok=False, numel=numel, stress_exchanges=0,
+                fallback="RCCL: peer-memory export/map unavailable on some rank")
         return None
     ts = TwoShot(comm, numel, tuple(regions), peers, timeout_s)
     comm.barrier()
     ok = ts.self_test() if test else True
-    if not all(comm.allgather(bool(ok))):
+    verdicts = comm.allgather(bool(ok))
+    if not all(verdicts):
         ts.close()
+        _record(comm, "two-shot", ok=False, numel=numel, stress_exchanges=0,
+                fallback=f"RCCL: stress self-test failed on rank(s) "
+                         f"{[r for r, v in enumerate(verdicts) if not v]}")
         return None
+    _record(comm, "two-shot", ok=True, numel=numel,
+            stress_exchanges=STRESS_REPS if test else 0, fallback=None)
     return ts

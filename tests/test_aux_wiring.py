@@ -122,34 +122,49 @@ def test_fingerprint_env_wraps_world():
 
 # ------------------------------------------------------------------ checkpoint commit
 def _ckpt_body(rank, size, path):
+    import glob
     comm = mg.get_world_comm()
     ckpt.save_optimizer_state(path, {"step": 5, "size": size, "x": torch.ones(2) * rank},
                               comm=comm, sharded=True)
-    st = ckpt.load_optimizer_state(path, rank=rank, sharded=True)
+    st = ckpt.load_optimizer_state(path, rank=rank, sharded=True, comm=comm)
     ckpt.check_loaded_step(st["step"], comm)
-    # an interrupted later checkpoint: rank 1's shard moves to step 9, the manifest does not
+    # an interrupted later checkpoint: rank 1 wrote its step-9 shard, the manifest was not
+    # committed -- the committed step-5 shards are untouched and still load everywhere
     comm.barrier()
     if rank == 1:
-        torch.save({"step": 9, "size": size}, ckpt.shard_path(path, 1))
+        torch.save({"step": 9, "size": size}, ckpt.shard_path(path, 1, 9))
+    comm.barrier()
+    st2 = ckpt.load_optimizer_state(path, rank=rank, sharded=True, comm=comm)
+    survived = st2["step"] == 5 and float(st2["x"][0]) == float(rank)
+    # a committed step whose shard is damaged on rank 1 only: EVERY rank raises
+    comm.barrier()
+    ckpt.save_optimizer_state(path, {"step": 7, "size": size, "x": torch.ones(2) * rank},
+                              comm=comm, sharded=True)
+    old = sorted(glob.glob(path + f".step[59].rank{rank}"))  # superseded shards removed
+    comm.barrier()
+    if rank == 1:
+        torch.save({"step": 6, "size": size}, ckpt.shard_path(path, 1, 7))
     comm.barrier()
     try:
-        ckpt.load_optimizer_state(path, rank=rank, sharded=True)
+        ckpt.load_optimizer_state(path, rank=rank, sharded=True, comm=comm)
         torn = False
-    except ckpt.CheckpointMismatch:
-        torn = True
+    except ckpt.CheckpointMismatch as e:
+        torn = "rank(s) [1]" in str(e)
     try:
         ckpt.check_loaded_step(5 + rank, comm)
         skew = False
     except ckpt.CheckpointMismatch:
         skew = True
-    return float(st["x"][0]), torn, skew
+    return float(st["x"][0]), survived, old, torn, skew
 
 
 def test_sharded_checkpoint_manifest(tmp_path):
-    res = run_distributed(_ckpt_body, 2, str(tmp_path / "opt.pt"))
-    assert res[0] == (0.0, False, True) and res[1] == (1.0, True, True)
-    man = json.loads(open(ckpt.manifest_path(str(tmp_path / "opt.pt"))).read())
-    assert man == {"step": 5, "size": 2, "sharded": True}
+    path = str(tmp_path / "opt.pt")
+    res = run_distributed(_ckpt_body, 2, path)
+    for r, (x, survived, old, torn, skew) in enumerate(res):
+        assert x == float(r) and survived and old == [] and torn and skew, res
+    man = json.loads(open(ckpt.manifest_path(path)).read())
+    assert man == {"step": 7, "size": 2, "sharded": True, "shards": "opt.pt.step7.rank{rank}"}
 
 
 # ------------------------------------------------------------------ two "nodes"

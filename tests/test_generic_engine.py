@@ -72,3 +72,84 @@ def test_generic_engine_gloo_ranks_match_single_rank(history):
         assert "collectives" in why
         np.testing.assert_allclose(traj, ref, rtol=2e-5, atol=1e-6)
     np.testing.assert_array_equal(res[0][0], res[1][0])
+
+
+# ------------------------------------------------------------- keys, aux, groups (CPU)
+class _Noisy(mg.OnePointModel):
+    """Stochastic model: the sumstats draw noise from the step's randkey on the model's
+    device (the engine's key contract: ``randkey.generator(device)``)."""
+
+    def calc_partial_sumstats_from_params(self, params, randkey=None):
+        t = self.aux_data["target"]
+        noise = 0.0
+        if randkey is not None:
+            noise = 0.3 * torch.randn(t.shape, generator=randkey.generator(t.device),
+                                      device=t.device)
+        return (params - t) ** 2 * (1.0 + noise)
+
+    def calc_loss_from_sumstats(self, sumstats, sumstats_aux=None, randkey=None):
+        return sumstats.sum()
+
+
+class _AuxModel(mg.OnePointModel):
+    """sumstats_func_has_aux: the aux (a per-rank weight) reaches the loss, unreduced."""
+
+    def calc_partial_sumstats_from_params(self, params, randkey=None):
+        t = self.aux_data["target"]
+        return (params - t) ** 2, self.aux_data["w"]
+
+    def calc_loss_from_sumstats(self, sumstats, sumstats_aux=None, randkey=None):
+        return (sumstats * sumstats_aux).sum()
+
+
+@pytest.mark.parametrize("const", [False, True])
+def test_generic_engine_randkey_matches_eager(const):
+    C.set_world_comm(None)
+    m = _Noisy(aux_data={"target": torch.tensor([1.0, -2.0, 0.5, 3.0])})
+    g0 = torch.zeros(4)
+    ref = m.run_adam(g0, nsteps=6, learning_rate=0.1, randkey=7, const_randkey=const,
+                     use_engine=False)
+    eng = GraphAdamEngine(m)
+    t = eng.run_adam(g0, nsteps=6, learning_rate=0.1, randkey=7, const_randkey=const)
+    torch.testing.assert_close(t, ref, rtol=0, atol=0)
+    noiseless = m.run_adam(g0, nsteps=6, learning_rate=0.1, use_engine=False)
+    assert not torch.equal(t, noiseless)
+
+
+def test_generic_engine_sumstats_aux_matches_eager():
+    C.set_world_comm(None)
+    m = _AuxModel(aux_data={"target": torch.tensor([1.0, -2.0, 0.5]),
+                            "w": torch.tensor([1.0, 2.0, 0.5])}, sumstats_func_has_aux=True)
+    ref = m.run_adam(torch.zeros(3), nsteps=5, learning_rate=0.1, use_engine=False)
+    t = GraphAdamEngine(m).run_adam(torch.zeros(3), nsteps=5, learning_rate=0.1)
+    torch.testing.assert_close(t, ref, rtol=0, atol=0)
+
+
+def _group_body(rank, size, engine):
+    comm = mg.get_world_comm()
+    sub, ngroups, gidx = mg.split_subcomms(num_groups=2, comm=comm)
+    # (no coordinate whose gradient cancels exactly between the groups: Adam would turn
+    # the summation-order residue of a zero into a full step)
+    tgt = torch.tensor([1.0, -2.0, 0.5]) if gidx == 0 else torch.tensor([-1.5, 0.5, 2.0])
+    m = _Noisy(aux_data={"target": tgt * (1 + sub.rank)}, comm=sub)
+    grp = mg.OnePointGroup(m, main_comm=comm)
+    if engine:
+        t = GraphAdamEngine(grp).run_adam(torch.zeros(3), nsteps=5, learning_rate=0.1,
+                                          randkey=3)
+    else:
+        t = grp.run_adam(torch.zeros(3), nsteps=5, learning_rate=0.1, randkey=3,
+                         use_engine=False)
+    lg = grp.calc_loss_and_grad_from_params(torch.tensor([0.1, 0.2, 0.3]))
+    return t.numpy(), float(lg[0]), lg[1].numpy()
+
+
+def test_generic_engine_group_matches_eager_group():
+    """OnePointGroup through the engine (members' chain rule on their sub-communicators,
+    one summed exchange on the main communicator) against the eager group path, 4 ranks
+    in 2 groups, per-step keys."""
+    eng = run_distributed(_group_body, 4, True)
+    ref = run_distributed(_group_body, 4, False)
+    for (t, l, g), (tr, lr, gr) in zip(eng, ref):
+        np.testing.assert_allclose(t, tr, rtol=1e-5, atol=1e-6)
+    for r in range(1, 4):
+        np.testing.assert_array_equal(eng[r][0], eng[0][0])

@@ -196,3 +196,123 @@ def test_two_ranks_uncapturable_hooks_fall_back_together(mode):
     assert not res[0][1] and not res[1][1]
     assert "rank 1" in res[0][2] and "rank 1" in res[1][2]
     np.testing.assert_array_equal(res[0][0], res[1][0])
+
+
+# ------------------------------------------------ per-step keys, sumstat aux, groups
+def _stoch_pop(comm=None, npar=20_000, nhalo=400_000, seed=11):
+    from multigrad_amd.models.torch_population import StochasticTorchPopulationSMFModel
+    m, guess = _torch_pop(comm, npar, nhalo, seed)
+    return StochasticTorchPopulationSMFModel(aux_data=m.aux_data, comm=comm), guess
+
+
+@pytest.mark.parametrize("const", [False, True])
+def test_graph_engine_randkey_replays_fresh_keys(const):
+    """A stochastic model (halo-mass scatter drawn from randkey.generator(device)) through
+    the captured step: the generators are registered with the graph and seeded with each
+    step's key before its replay, so the trajectory equals the eager per-step-key loop's."""
+    from multigrad_amd.engine.generic import GraphAdamEngine
+    m, guess = _stoch_pop()
+    ref = m.run_adam(guess, nsteps=6, learning_rate=1e-3, randkey=5, const_randkey=const,
+                     use_engine=False)
+    eng = GraphAdamEngine(m, graph=True)
+    t = eng.run_adam(guess, nsteps=6, learning_rate=1e-3, randkey=5, const_randkey=const)
+    assert eng.use_graph and eng.graph is not None, eng.fallback_reason
+    torch.testing.assert_close(t, ref, rtol=1e-6, atol=1e-7)
+    t2 = m.run_adam(guess, nsteps=6, learning_rate=1e-3, randkey=5, const_randkey=const)
+    torch.testing.assert_close(t2, t, rtol=0, atol=0)      # the front-end routes here
+    if not const:  # the keys really change per step: a constant key gives another path
+        tc = m.run_adam(guess, nsteps=6, learning_rate=1e-3, randkey=5, const_randkey=True)
+        assert not torch.equal(tc, t)
+
+
+def test_graph_engine_host_key_use_falls_back():
+    from multigrad_amd.engine.generic import GraphAdamEngine
+    from multigrad_amd.models.torch_population import StochasticTorchPopulationSMFModel
+
+    class HostKey(StochasticTorchPopulationSMFModel):
+        def calc_partial_sumstats_from_params(self, params, randkey=None):
+            _ = randkey.value  # a host integer: cannot be replayed with a fresh key
+            return super().calc_partial_sumstats_from_params(params, randkey)
+
+    m, guess = _stoch_pop()
+    h = HostKey(aux_data=m.aux_data)
+    ref = h.run_adam(guess, nsteps=4, learning_rate=1e-3, randkey=2, use_engine=False)
+    eng = GraphAdamEngine(h)
+    t = eng.run_adam(guess, nsteps=4, learning_rate=1e-3, randkey=2)
+    assert not eng.use_graph and "randkey.value" in eng.fallback_reason
+    torch.testing.assert_close(t, ref, rtol=1e-6, atol=1e-7)
+
+
+def _keys_two(rank, size, engine):
+    os.environ["MULTIGRAD_GENERIC_ENGINE"] = "1" if engine else "0"
+    import multigrad_amd as mg
+    from multigrad_amd.engine.generic import GraphAdamEngine
+    comm = mg.get_world_comm()
+    m, guess = _stoch_pop(comm, npar=8000, nhalo=200_000)
+    if engine:
+        eng = GraphAdamEngine(m, graph=True)
+        t = eng.run_adam(guess, nsteps=5, learning_rate=1e-3, randkey=9)
+        return t.cpu().numpy(), eng.use_graph
+    return m.run_adam(guess, nsteps=5, learning_rate=1e-3, randkey=9).cpu().numpy(), False
+
+
+def test_graph_engine_randkey_two_ranks_bitwise():
+    """Two ranks on one GPU, per-step keys inside the captured step (one-shot sumstats,
+    two-shot Adam exchange): bitwise the same trajectory on both ranks, equal to the
+    eager two-rank loop."""
+    eng = run_distributed(_keys_two, 2, True, timeout=600)
+    ref = run_distributed(_keys_two, 2, False, timeout=600)
+    assert eng[0][1] and eng[1][1]
+    np.testing.assert_array_equal(eng[0][0], eng[1][0])
+    np.testing.assert_allclose(eng[0][0], ref[0][0], rtol=1e-5, atol=1e-6)
+
+
+def test_graph_engine_sumstats_aux():
+    from multigrad_amd.engine.generic import GraphAdamEngine
+    from multigrad_amd.models.torch_population import TorchPopulationSMFModel
+
+    class WithAux(TorchPopulationSMFModel):
+        def calc_partial_sumstats_from_params(self, params, randkey=None):
+            s = super().calc_partial_sumstats_from_params(params)
+            return s, self.aux_data["w"]
+
+        def calc_loss_from_sumstats(self, sumstats, sumstats_aux=None, randkey=None):
+            return super().calc_loss_from_sumstats(sumstats * sumstats_aux)
+
+    m, guess = _torch_pop()
+    aux = dict(m.aux_data, w=torch.linspace(0.8, 1.2, 10, device=DEV))
+    w = WithAux(aux_data=aux, sumstats_func_has_aux=True)
+    ref = w.run_adam(guess, nsteps=5, learning_rate=1e-3, use_engine=False)
+    eng = GraphAdamEngine(w, graph=True)
+    t = eng.run_adam(guess, nsteps=5, learning_rate=1e-3)
+    assert eng.use_graph
+    torch.testing.assert_close(t, ref, rtol=1e-6, atol=1e-7)
+
+
+def _group_two(rank, size, engine):
+    os.environ["MULTIGRAD_GENERIC_ENGINE"] = "1" if engine else "0"
+    import multigrad_amd as mg
+    from multigrad_amd.engine.generic import GraphAdamEngine
+    comm = mg.get_world_comm()
+    sub, ng, gidx = mg.split_subcomms(num_groups=2, comm=comm)
+    m, guess = _torch_pop(sub, npar=8000, nhalo=150_000, seed=11 + gidx)
+    grp = mg.OnePointGroup(m, main_comm=comm)
+    if engine:
+        eng = GraphAdamEngine(grp, graph=True)
+        t = eng.run_adam(guess, nsteps=5, learning_rate=1e-3)
+        return t.cpu().numpy(), eng.use_graph, eng.last_loss()
+    t = grp.run_adam(guess, nsteps=5, learning_rate=1e-3)
+    return t.cpu().numpy(), False, None
+
+
+def test_graph_engine_group_two_groups():
+    """A 2-group OnePointGroup (one population model per rank, each on its own
+    sub-communicator) through ONE captured step per iteration: member chain rules, the
+    group loss over a 1-float one-shot and the two-shot Adam exchange over the main
+    communicator; same bits on both ranks, equal to the eager group loop."""
+    eng = run_distributed(_group_two, 2, True, timeout=600)
+    ref = run_distributed(_group_two, 2, False, timeout=600)
+    assert eng[0][1] and eng[1][1]
+    np.testing.assert_array_equal(eng[0][0], eng[1][0])
+    assert eng[0][2] == eng[1][2]
+    np.testing.assert_allclose(eng[0][0], ref[0][0], rtol=1e-5, atol=1e-6)

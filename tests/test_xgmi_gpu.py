@@ -172,3 +172,40 @@ def _engine_err(rank, size):
 def test_engine_raises_on_exchange_error():
     r0, r1 = run_distributed(_engine_err, 2, timeout=300)
     assert r0 == [True, True, True, True] and r1 == [False, False, True, True]
+
+
+# ------------------------------------------------ connect-time stress self-tests (2 / 8 ranks)
+def _stress(rank, size, corrupt):
+    import os
+    if corrupt:
+        os.environ["MULTIGRAD_XGMI_SELFTEST_CORRUPT"] = "1"
+    import multigrad_amd as mg
+    from multigrad_amd.parallel.xgmi import STRESS_REPS, connect, connect_twoshot, status
+    comm = mg.get_world_comm()
+    one = connect(comm, timeout_s=20.0)
+    two = connect_twoshot(comm, 4 * size * 4096, timeout_s=20.0)
+    got = (one is not None, two is not None)
+    for ctx in (one, two):
+        if ctx is not None:
+            ctx.close()
+    torch.cuda.synchronize()
+    return got, status(comm), STRESS_REPS
+
+
+@pytest.mark.parametrize("size", [2, 8])
+def test_stress_selftest_passes_and_corruption_falls_back(size):
+    """The connect-time self-tests run 32 back-to-back device-only exchanges with
+    step-unique values, one verification at the end: they pass on 2 and 8 processes
+    sharing the GPU; a rank that corrupts its slice in one exchange (test hook) makes every
+    rank fail them and fall back to RCCL, with the reason recorded."""
+    ok = run_distributed(_stress, size, False, timeout=600)
+    for got, st, reps in ok:
+        assert got == (True, True), st
+        assert st["one-shot"][-1]["ok"] and st["one-shot"][-1]["stress_exchanges"] == reps >= 32
+        assert st["two-shot"][-1]["ok"] and st["two-shot"][-1]["stress_exchanges"] == reps
+    bad = run_distributed(_stress, size, True, timeout=600)
+    for got, st, reps in bad:
+        assert got == (False, False), st
+        for kind in ("one-shot", "two-shot"):
+            e = st[kind][-1]
+            assert not e["ok"] and "stress self-test failed" in e["fallback"] and "RCCL" in e["fallback"]
