@@ -208,6 +208,9 @@ class GraphAdamEngine:
             self.m_oneshot = [get_oneshot(md.comm) if md.comm is not None and md.comm.size > 1
                               else None for md in self.members]
         self.P_pad = P_pad if self.twoshot is not None else P
+        # which dense-gradient exchange the run uses (kept after close())
+        self.grad_exchange = ("none" if W == 1 else "two-shot" if self.twoshot is not None
+                              else "two-shot all-reduce" if self.ar is not None else "rccl/gloo")
         f32 = dict(dtype=torch.float32, device=dev)
         # the hooks read p (cached memory); with the two-shot exchange the parameters live
         # in its uncached peer-memory region and p is refreshed from it after each step

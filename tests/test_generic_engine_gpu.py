@@ -73,7 +73,8 @@ def _two_ranks(rank, size, graph):
     m, guess = _torch_pop(comm, npar=8000, nhalo=200_000)
     eng = GraphAdamEngine(m)
     traj = eng.run_adam(guess, nsteps=5, learning_rate=1e-3)
-    return traj.cpu().numpy(), eng.use_graph, eng.twoshot is not None, eng.oneshot is not None
+    return traj.cpu().numpy(), eng.use_graph, eng.grad_exchange == "two-shot", \
+        eng.m_oneshot[0] is not None
 
 
 def test_graph_engine_two_ranks_peer_memory_collectives():
@@ -296,6 +297,7 @@ def _group_two(rank, size, engine):
     comm = mg.get_world_comm()
     sub, ng, gidx = mg.split_subcomms(num_groups=2, comm=comm)
     m, guess = _torch_pop(sub, npar=8000, nhalo=150_000, seed=11 + gidx)
+    guess = comm.bcast(guess.cpu(), root=0).to(DEV)  # the group shares ONE parameter vector
     grp = mg.OnePointGroup(m, main_comm=comm)
     if engine:
         eng = GraphAdamEngine(grp, graph=True)
