@@ -1,7 +1,12 @@
 """Generic-model Adam on one MI355X: the population SMF model written in plain torch ops
 (``models/torch_population.py``): eager distributed chain rule + run_adam (a Python loop
 of torch launches), the generic engine forced to replay one HIP graph per step, and the
-default front-end path (the generic engine's auto policy).  One JSON line per path."""
+default front-end path (the generic engine's auto policy).  One JSON line per path.
+
+``--model``: ``plain`` (deterministic), ``randkey`` (the stochastic variant: halo-mass
+scatter drawn from a fresh key every step, reference multigrad/adam.py:59-62), or
+``group`` (a 2-member OnePointGroup of population models, reference
+multigrad/multigrad.py:547-607, both members on this rank)."""
 import argparse
 import json
 import os
@@ -19,36 +24,54 @@ def main(argv=None):
     ap.add_argument("--params", type=int, default=1_000_000)
     ap.add_argument("--halos", type=int, default=10_000_000)
     ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--model", default="plain", choices=["plain", "randkey", "group"])
     a = ap.parse_args(argv)
     from multigrad_amd.engine.generic import GraphAdamEngine
     from multigrad_amd.models.population import PopulationSMFModel, make_population_data
-    from multigrad_amd.models.torch_population import TorchPopulationSMFModel, torch_population_data
+    from multigrad_amd.models.onepoint import OnePointGroup
+    from multigrad_amd.models.torch_population import (StochasticTorchPopulationSMFModel,
+                                                       TorchPopulationSMFModel,
+                                                       torch_population_data)
     dev = torch.device("cuda", 0)
-    data = make_population_data(a.params, a.halos, seed=5, device=dev)
-    PopulationSMFModel(aux_data=data).set_target_from_truth()
-    m = TorchPopulationSMFModel(aux_data=torch_population_data(data))
-    guess = data["guess"]
+
+    def member(seed):
+        data = make_population_data(a.params, a.halos, seed=seed, device=dev)
+        PopulationSMFModel(aux_data=data).set_target_from_truth()
+        cls = StochasticTorchPopulationSMFModel if a.model == "randkey" else TorchPopulationSMFModel
+        return cls(aux_data=torch_population_data(data)), data["guess"]
+
+    m, guess = member(5)
+    if a.model == "group":
+        m = OnePointGroup((m, member(6)[0]))
+    kw = dict(learning_rate=1e-3)
+    if a.model == "randkey":
+        kw["randkey"] = 7
     out = {}
     tuned = {}
 
     def _auto(n):
         eng = GraphAdamEngine(m)
-        traj = eng.run_adam(guess, nsteps=n, learning_rate=1e-3)
+        traj = eng.run_adam(guess, nsteps=n, **kw)
         tuned.update(eng.tuning or {"fallback": eng.fallback_reason})
         return traj
-    for name, fn in (("eager", lambda n: m.run_adam(guess, nsteps=n, learning_rate=1e-3,
-                                                    use_engine=False)),
+    for name, fn in (("eager", lambda n: m.run_adam(guess, nsteps=n, use_engine=False, **kw)),
                      ("graph", lambda n: GraphAdamEngine(m, graph=True).run_adam(
-                         guess, nsteps=n, learning_rate=1e-3)),
+                         guess, nsteps=n, **kw)),
                      ("auto", lambda n: _auto(n))):
-        fn(3)  # warm-up (kernel loading, capture)
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        traj = fn(a.steps)
-        torch.cuda.synchronize()
-        dt = time.perf_counter() - t0
+        fn(3)  # warm-up (kernel loading)
+        # marginal cost per step: (t(2K) - t(K)) / K, so engine setup and capture (a fixed
+        # cost per run) do not count against the steps
+        ts = []
+        for n in (a.steps, 2 * a.steps):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            traj = fn(n)
+            torch.cuda.synchronize()
+            ts.append(time.perf_counter() - t0)
+        dt = ts[1] - ts[0]
         out[name] = a.steps / dt
-        print(json.dumps({"config": f"generic-torch-population-{a.params:.0e}param", "path": name,
+        print(json.dumps({"config": f"generic-torch-population-{a.params:.0e}param-{a.model}",
+                          "path": name, "setup_s": round(ts[0] - dt, 4),
                           "steps_per_s": round(a.steps / dt, 2), "halos": a.halos,
                           "final_param_0": float(traj[-1, 0])}), flush=True)
     print(json.dumps({"graph_speedup": round(out["graph"] / out["eager"], 3),

@@ -556,6 +556,7 @@ class FusedAdamEngine:
             release_twoshot(self.comm, self._ts_keep)
         self._ts_keep = None
         self.twoshot = None
+        self.graph = None
         self.ready = False
 
     def _twoshot_update(self, c: int):
@@ -826,6 +827,9 @@ class FusedAdamEngine:
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         torch.cuda.current_stream().wait_stream(s)
+        import gc
+        self.graph = None
+        gc.collect()  # an unreferenced CUDAGraph freed during a capture aborts the process
         self.graph = torch.cuda.CUDAGraph()
         self._capturing = True
         try:

@@ -303,6 +303,10 @@ class GraphAdamEngine:
             from ..parallel.xgmi import release_twoshot
             release_twoshot(self.comm, self.twoshot)
         self.twoshot = None
+        # destroy the graph now: a CUDAGraph that the garbage collector happens to free
+        # while another graph is being captured aborts the process (hipGraphExecDestroy
+        # is not permitted on a capturing stream)
+        self.graph = None
         self.ready = False
 
     # ------------------------------------------------------------------ the step
@@ -367,6 +371,8 @@ class GraphAdamEngine:
                             f"sumstats of {n} x {dt} do not fit the capturable one-shot "
                             f"all-reduce (fp32, <= {MAX_FLOATS} values)")
             if capture:
+                import gc
+                gc.collect()  # see _capture
                 g = torch.cuda.CUDAGraph()
                 for gen in self._gens:
                     g.register_generator_state(gen)
@@ -498,6 +504,8 @@ class GraphAdamEngine:
             self.traj_loc[1].copy_(traj_saved)
         if hist_saved is not None:
             self.history.buf[1].copy_(hist_saved)
+        import gc
+        gc.collect()  # no unreferenced CUDAGraph may be freed during the capture
         graph = torch.cuda.CUDAGraph()
         for gen in self._gens:
             graph.register_generator_state(gen)
