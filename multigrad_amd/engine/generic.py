@@ -514,8 +514,24 @@ class GraphAdamEngine:
         return graph
 
     def _replay(self, key) -> None:
+        """Replay the captured step.  A step with graph-registered generators is replayed
+        on the engine's own stream, ordered after the current stream by an event and back:
+        launched on the default stream right after a host synchronisation, such a graph
+        computed wrong sums downstream of its RNG op on this ROCm runtime (the RNG output
+        itself was right), reproducibly, while the side-stream launch matched the eager
+        step bit for bit with and without synchronisation (tools/dbg/auto_keys10.py,
+        docs/design.md)."""
         self._seed_generators(key)
-        self.graph.replay()
+        if not self._gens:
+            self.graph.replay()
+            return
+        cur = torch.cuda.current_stream()
+        if getattr(self, "_rs", None) is None:
+            self._rs = torch.cuda.Stream()
+        self._rs.wait_stream(cur)
+        with torch.cuda.stream(self._rs):
+            self.graph.replay()
+        cur.wait_stream(self._rs)
 
     _TUNE = 3  # steps timed per mode by the auto policy
 

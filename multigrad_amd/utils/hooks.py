@@ -1,5 +1,7 @@
-"""Per-step driver hooks: the aux subsystems of SURVEY §5.2/§5.3/§5.5 wired into every
-optimizer loop (Adam, the fused engine, simple GD, L-BFGS, in-graph GD).
+"""Per-step driver hooks: the aux subsystems of SURVEY §5.2/§5.3/§5.5 wired into the
+optimizer loops -- Adam, the fused and generic engines, simple GD, in-graph GD (eager
+steps), device L-BFGS and device L-BFGS-B (metrics also on the root of the scipy
+L-BFGS-B; its workers run no loop of their own).
 
 Environment knobs (read when a driver starts):
 

@@ -318,3 +318,23 @@ def test_graph_engine_group_two_groups():
     np.testing.assert_array_equal(eng[0][0], eng[1][0])
     assert eng[0][2] == eng[1][2]
     np.testing.assert_allclose(eng[0][0], ref[0][0], rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("graph", [True, None])
+def test_graph_engine_randkey_with_host_syncs(graph):
+    """Keyed captured steps with a host synchronisation between replays (a user callback,
+    and the auto policy's timing windows): the replays still equal the eager steps.
+    Launched on the default stream right after a sync, a graph with an RNG op computed
+    wrong sums downstream of it on this runtime; the engine replays keyed graphs on its
+    own stream (GraphAdamEngine._replay)."""
+    from multigrad_amd.engine.generic import GraphAdamEngine
+    m, guess = _stoch_pop()
+    ref = m.run_adam(guess, nsteps=10, learning_rate=1e-3, randkey=7, use_engine=False)
+
+    def sync(i, loss, state):
+        torch.cuda.synchronize()
+
+    eng = GraphAdamEngine(m, graph=graph)
+    t = eng.run_adam(guess, nsteps=10, learning_rate=1e-3, randkey=7, callback=sync)
+    assert eng.use_graph or graph is None
+    torch.testing.assert_close(t, ref, rtol=0, atol=0)
