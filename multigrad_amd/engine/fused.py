@@ -556,7 +556,6 @@ class FusedAdamEngine:
             release_twoshot(self.comm, self._ts_keep)
         self._ts_keep = None
         self.twoshot = None
-        self.graph = None
         self.ready = False
 
     def _twoshot_update(self, c: int):
@@ -827,14 +826,14 @@ class FusedAdamEngine:
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         torch.cuda.current_stream().wait_stream(s)
-        import gc
+        from .generic import _no_gc
         self.graph = None
-        gc.collect()  # an unreferenced CUDAGraph freed during a capture aborts the process
         self.graph = torch.cuda.CUDAGraph()
         self._capturing = True
         try:
-            with torch.cuda.graph(self.graph):
-                self._enqueue_step()
+            with _no_gc():  # no CUDAGraph may be freed by the collector during a capture
+                with torch.cuda.graph(self.graph):
+                    self._enqueue_step()
         finally:
             self._capturing = False
 

@@ -92,6 +92,24 @@ class _CaptureKey:
             f"can be replayed with a fresh key per step")
 
 
+class _no_gc:
+    """Collect garbage now and keep the cyclic collector off during a graph capture: a
+    CUDAGraph freed by the collector while another graph is being captured aborts the
+    process (hipGraphExecDestroy is not permitted on a capturing stream)."""
+
+    def __enter__(self):
+        import gc
+        gc.collect()
+        self._was = gc.isenabled()
+        gc.disable()
+
+    def __exit__(self, *exc):
+        import gc
+        if self._was:
+            gc.enable()
+        return False
+
+
 def _leaf_view(p: torch.Tensor, shape) -> torch.Tensor:
     return p.detach().view(shape).requires_grad_(True)
 
@@ -303,10 +321,6 @@ class GraphAdamEngine:
             from ..parallel.xgmi import release_twoshot
             release_twoshot(self.comm, self.twoshot)
         self.twoshot = None
-        # destroy the graph now: a CUDAGraph that the garbage collector happens to free
-        # while another graph is being captured aborts the process (hipGraphExecDestroy
-        # is not permitted on a capturing stream)
-        self.graph = None
         self.ready = False
 
     # ------------------------------------------------------------------ the step
@@ -371,13 +385,12 @@ class GraphAdamEngine:
                             f"sumstats of {n} x {dt} do not fit the capturable one-shot "
                             f"all-reduce (fp32, <= {MAX_FLOATS} values)")
             if capture:
-                import gc
-                gc.collect()  # see _capture
                 g = torch.cuda.CUDAGraph()
                 for gen in self._gens:
                     g.register_generator_state(gen)
-                with torch.cuda.graph(g):
-                    self._hooks_only(key)
+                with _no_gc():
+                    with torch.cuda.graph(g):
+                        self._hooks_only(key)
                 del g
         except Exception as exc:  # noqa: BLE001  (host sync / dynamic shapes in user code)
             torch.cuda.synchronize()
@@ -504,13 +517,12 @@ class GraphAdamEngine:
             self.traj_loc[1].copy_(traj_saved)
         if hist_saved is not None:
             self.history.buf[1].copy_(hist_saved)
-        import gc
-        gc.collect()  # no unreferenced CUDAGraph may be freed during the capture
         graph = torch.cuda.CUDAGraph()
         for gen in self._gens:
             graph.register_generator_state(gen)
-        with torch.cuda.graph(graph):
-            self._body(None, key)
+        with _no_gc():
+            with torch.cuda.graph(graph):
+                self._body(None, key)
         return graph
 
     def _replay(self, key) -> None:
