@@ -57,6 +57,16 @@ struct Tile {
   int32_t pad;
 };
 
+// Edge-pair layout of the packed-fp32 kernels: edges (2i, 2i+1) form pair i; with an odd
+// edge count the last edge gets a pair of its own (.x used).
+template <int NB>
+struct EdgePairs {
+  static constexpr int NE = NB + 1;
+  static constexpr int NP = NE / 2;             // pairs inside one halo
+  static constexpr int NX = NE & 1;             // 1: cross-halo pair for the last edge
+  static constexpr int NV = NP + NX;            // accumulator pairs
+};
+
 template <bool LOGSIG>
 __device__ __forceinline__ float inv_sigma(float s) {
   return LOGSIG ? fast_exp2(-s * kLog2_10) : 1.0f / s;
@@ -116,17 +126,23 @@ __device__ __forceinline__ const float4* tail_tab_lane(const float4* tab) {
 // counts; the per-bin differences are formed once per thread at the end.
 // A halo with x = -inf contributes exactly zero (used to mask the unrolled tail): every
 // V_e is -0 and every pos_e is 1, which cancels in the differences.
+#ifndef MG_FWD_TAB_FOLD
+#define MG_FWD_TAB_FOLD 1
+#endif
 template <int NB, bool LOGSIG, bool REL, int REPL = 0>
 __device__ __forceinline__ void halo_mass(float x, float2 th, const SmfBins& b,
                                           float (&acc)[NB + 1], int (&cnt)[NB + 1],
                                           const float4* __restrict__ tb = nullptr) {
-  const float ninv = -inv_sigma<LOGSIG>(th.y) * kWScale;
-  const float mu = -(x + th.x) * ninv;  // = (x + a) * kWScale / sigma
+  // table path: the coordinate is formed directly in table units (the piece scale folded
+  // into the two per-halo factors: one multiply per halo instead of one per edge)
+  constexpr bool kFold = REPL > 0 && MG_FWD_TAB_FOLD;
+  const float ninv = -inv_sigma<LOGSIG>(th.y) * (kFold ? kWScale * kTailTabInvH : kWScale);
+  const float mu = -(x + th.x) * ninv;  // = (x + a) * kWScale / sigma (x kTailTabInvH)
 #pragma unroll
   for (int e = 0; e <= NB; ++e) {
     const float n = fmaf(b.edge[e], ninv, mu);
     if constexpr (REPL > 0) {  // signed-tail table (see ep_eval_tab)
-      const float t = __builtin_amdgcn_fmed3f(n * kTailTabInvH, -(float)(kTailTabN / 2),
+      const float t = __builtin_amdgcn_fmed3f(kFold ? n : n * kTailTabInvH, -(float)(kTailTabN / 2),
                                               (float)(kTailTabN / 2) - 1.0f / 4096);
       const float4 c = tb[cvt_flr_i32(t) * REPL];
       const float s = __builtin_amdgcn_fractf(t);
@@ -698,13 +714,7 @@ __device__ __forceinline__ void lane_halo2(v2f x, float ninv, float mua, const S
 // pair (its accumulators keep one partial per halo, folded once at the end).
 // Packed per pair: the edge fma, w^2, the Horner chain, the accumulate and both residual
 // updates; per element: |w|+K, v_rcp, v_exp, the sign (v_bfi) and the count compare.
-template <int NB>
-struct EdgePairs {
-  static constexpr int NE = NB + 1;
-  static constexpr int NP = NE / 2;             // pairs inside one halo
-  static constexpr int NX = NE & 1;             // 1: cross-halo pair for the last edge
-  static constexpr int NV = NP + NX;            // accumulator pairs
-};
+// (EdgePairs<NB>: the edge-pair layout, defined at the top of the file)
 
 template <int NB, bool REL, bool RESID>
 __device__ __forceinline__ void ep_eval(v2f n, v2f (&acc)[EdgePairs<NB>::NV],
@@ -1009,6 +1019,267 @@ __device__ __forceinline__ void em_group_end(const EmLane& L, v2f (&F)[EdgePairs
       accp[i].x += C;
     }
   }
+}
+
+// ================================================= tiles VJP, recurrence + owner segments
+// MG_VJP_REC (default on, uniform unpadded bins): the tiles VJP of the hashed shards with
+// (1) the Gaussian factors of one halo's equally spaced edges from one seed pair at the
+//     middle edges and the exact ratio recurrence f_{e+2} = f_e exp2(-4 dw w_{e+1}) (the
+//     ratio itself advances by the constant exp2(-8 dw^2)): 6 transcendentals per halo
+//     instead of 12, two v_pk_fma per edge pair for the sums A = sum h_e f_e and
+//     D = sum (e - 2M) h_e f_e, and B = sum h_e f_e w_e = w_{2M} A + dw D by linearity;
+// (2) per-halo contributions already in gradient units (every halo of a population
+//     shares its inverse sigma), so a population's gradient is the plain sum of its
+//     halos' contributions; and
+// (3) no block-wide scan: after the coalesced per-halo pass, each thread walks 8
+//     consecutive halos; the thread holding a population's FIRST halo owns it, adds the
+//     head partials of the following threads it continues into (fixed order: bitwise
+//     reproducible), writes the gradient straight to HBM and zero-fills the ids up to the
+//     next population present (populations without halos on this rank).
+// The seed sits at the middle pair, so a seed that underflows (|z| > 13) is at least
+// 13 - NB/2 h sigma away from every edge; with h = delta/sigma <= 1 (dw <= kWScale, checked
+// wave-uniformly, else the per-edge path of halo_vjp) the dropped terms are below 3e-15.
+#ifndef MG_VJP_REC
+#define MG_VJP_REC 1
+#endif
+
+template <int NB>
+struct VjpPairs {
+  v2f h[EdgePairs<NB>::NV];  // h_e in the edge-pair layout (odd last edge in .x of the extra pair)
+  v2f d[EdgePairs<NB>::NV];  // (e - 2M) h_e
+};
+
+// One halo: A = sum_e h_e f_e, D = sum_e (e - 2M) h_e f_e, wc = w_{2M}; nm = -(x + a) inv.
+template <int NB>
+__device__ __forceinline__ void halo_vjp_rec(float nm, float inv, float dw, const VjpPairs<NB>& W,
+                                             const SmfBins& b, float& A, float& D, float& wc) {
+  using EP = EdgePairs<NB>;
+  constexpr int M = EP::NP / 2;
+  v2f e2;
+  e2.x = b.edge[2 * M];
+  e2.y = b.edge[2 * M + 1];
+  const v2f ws = e2 * inv + nm;
+  const v2f q = -ws * ws;
+  v2f p0;
+  p0.x = fast_exp2(q.x);
+  p0.y = fast_exp2(q.y);
+  const float dw4 = -4.0f * dw;
+  const float C2 = fast_exp2(dw4 * dw);  // exp2(-4 dw^2): ratio of the two halves of a pair
+  const float C4 = C2 * C2;              // per-pair advance of the ratio
+  v2f Af = W.h[M] * p0, Df = W.d[M] * p0;
+  v2f R;
+  R.x = fast_exp2(__builtin_amdgcn_fmed3f(dw4 * ws.y, -126.0f, 126.0f));
+  R.y = R.x * C2;
+  v2f p = p0;
+#pragma unroll
+  for (int i = M + 1; i < EP::NP; ++i) {
+    p = p * R;
+    Af = W.h[i] * p + Af;
+    Df = W.d[i] * p + Df;
+    R = R * C4;
+  }
+  if constexpr (EP::NX) {
+    const float f = p.x * R.x;
+    Af.x = fmaf(W.h[EP::NP].x, f, Af.x);
+    Df.x = fmaf(W.d[EP::NP].x, f, Df.x);
+  }
+  if constexpr (M > 0) {
+    v2f Rb;
+    Rb.y = fast_exp2(__builtin_amdgcn_fmed3f(-dw4 * ws.x, -126.0f, 126.0f));
+    Rb.x = Rb.y * C2;
+    p = p0;
+#pragma unroll
+    for (int i = M - 1; i >= 0; --i) {
+      p = p * Rb;
+      Af = W.h[i] * p + Af;
+      Df = W.d[i] * p + Df;
+      Rb = Rb * C4;
+    }
+  }
+  A = Af.x + Af.y;
+  D = Df.x + Df.y;
+  wc = ws.x;
+}
+
+template <int NB, bool LOGSIG>
+#ifndef MG_VJP_REC_MINWAVES
+#define MG_VJP_REC_MINWAVES 8  // 20 KB of LDS and <= 64 VGPRs: 8 workgroups per CU
+#endif
+__global__ __launch_bounds__(kThreads, MG_VJP_REC_MINWAVES) void smf_vjp_tiles_rec_kernel(
+    const float* __restrict__ x, const int32_t* __restrict__ pop,
+    const float2* __restrict__ theta, const Tile* __restrict__ tiles,
+    const float* __restrict__ hvec, SmfBins bins, float2* __restrict__ grad,
+    float2* __restrict__ partials) {
+  using EP = EdgePairs<NB>;
+  constexpr int M = EP::NP / 2;
+  // LDS (20 KB, so 8 workgroups fit a CU): per-halo contributions (later the per-population
+  // results) and local population ids (later the head partials and their successors)
+  __shared__ __attribute__((aligned(16))) char smem[kTileHalos * (sizeof(float2) + sizeof(int16_t))];
+  const Tile t = tiles[blockIdx.x];
+  const int tid = threadIdx.x;
+  if (t.slot >= 0) {  // partial tile (one giant population): the per-edge block reduction
+    float h[NB + 1];
+#pragma unroll
+    for (int e = 0; e <= NB; ++e) h[e] = hvec[e];
+    const float2 th = theta[t.p0];
+    const float inv = inv_sigma<LOGSIG>(th.y) * kWScale;
+    float v[2] = {0.0f, 0.0f};
+    for (int64_t i = t.h0 + tid; i < t.h1; i += kThreads)
+      halo_vjp<NB, LOGSIG>(x[i], th, inv, h, bins, v[0], v[1]);
+    block_sum_n<2>(v, reinterpret_cast<float*>(smem));
+    if (tid == 0) partials[t.slot] = make_float2(v[0], v[1]);
+    return;
+  }
+  const int n = (int)(t.h1 - t.h0);
+  const int npops = t.p1 - t.p0;
+  float2* __restrict__ gout = grad + t.p0;
+  if (n <= 0) {  // populations without halos on this rank
+    for (int k = tid; k < npops; k += kThreads) gout[k] = make_float2(0.f, 0.f);
+    return;
+  }
+  VjpPairs<NB> W;
+#pragma unroll
+  for (int i = 0; i < EP::NV; ++i) {
+    const int e0 = 2 * i, e1 = 2 * i + 1;
+    W.h[i].x = hvec[e0];
+    W.h[i].y = e1 <= NB ? hvec[e1] : 0.0f;
+    W.d[i].x = (float)(e0 - 2 * M) * W.h[i].x;
+    W.d[i].y = (float)(e1 - 2 * M) * W.h[i].y;
+  }
+  // s_g: per-halo contributions, 16-byte slot s (halos 2s, 2s+1) stored at slot
+  // swz(s) = s ^ ((s >> 4) & 3): thread t's blocked read of slots 4t..4t+3 then hits 16
+  // distinct bank slots per ds_read_b128 lane group (t mod 4 x (t >> 2) mod 4), and the
+  // striped phase-1 writes stay contiguous per 8 slots.  s_lp: local ids, plain order.
+  float2* s_g = reinterpret_cast<float2*>(smem);
+  int16_t* s_lp = reinterpret_cast<int16_t*>(smem + kTileHalos * sizeof(float2));
+  float2* res = s_g;                                      // per-population results (phase 2)
+  float2* s_head = reinterpret_cast<float2*>(s_lp);       // head partials (phase 2)
+  int* s_pass = reinterpret_cast<int*>(s_head + kThreads);
+  static_assert(kThreads * (sizeof(float2) + sizeof(int)) <= kTileHalos * sizeof(int16_t),
+                "head partials alias the id array");
+  static_assert(kTileHalos == kTilePops, "result array aliases the contribution array");
+  auto swz = [](int i) { return i ^ (((i >> 5) & 3) << 1); };  // halo index -> float2 index
+  // ---- phase 1: coalesced loads, per-halo gradient contributions in halo order
+  {
+    float xs[kItems];
+    int ps[kItems];
+    float2 ths[kItems];
+    // uniform tile base + clamped 32-bit offsets (always valid addresses, no branches)
+    const float* __restrict__ xt = x + t.h0;
+    const int32_t* __restrict__ pt = pop + t.h0;
+#pragma unroll
+    for (int r = 0; r < kItems; ++r) {
+      const int i = min(r * kThreads + tid, n - 1);
+      xs[r] = xt[i];
+      ps[r] = pt[i];
+    }
+#pragma unroll
+    for (int r = 0; r < kItems; ++r) ths[r] = theta[ps[r]];
+    bool ok = true;
+#pragma unroll
+    for (int r = 0; r < kItems; ++r) ok = ok && bins.delta * inv_sigma<LOGSIG>(ths[r].y) <= 1.0f;
+    constexpr float kInvW = 1.0f / kWScale;
+    if (__builtin_amdgcn_ballot_w64(!ok) == 0) {  // wave-uniform: the recurrence for all 8
+#pragma unroll
+      for (int r = 0; r < kItems; ++r) {
+        const float is = inv_sigma<LOGSIG>(ths[r].y);
+        const float inv = is * kWScale;
+        const float dw = bins.delta * inv;
+        float A, D, wc;
+        halo_vjp_rec<NB>(-(xs[r] + ths[r].x) * inv, inv, dw, W, bins, A, D, wc);
+        const float B = fmaf(wc, A, dw * D);
+        const int li = r * kThreads + tid;
+        s_g[swz(li)] = make_float2(-is * A, LOGSIG ? -(kLn10 * kInvW) * B : -(is * kInvW) * B);
+        s_lp[li] = (int16_t)(ps[r] - t.p0);
+      }
+    } else {
+      float h[NB + 1];
+#pragma unroll
+      for (int e = 0; e <= NB; ++e) h[e] = hvec[e];
+#pragma unroll
+      for (int r = 0; r < kItems; ++r) {
+        const float is = inv_sigma<LOGSIG>(ths[r].y);
+        float A = 0.f, B = 0.f;
+        halo_vjp<NB, LOGSIG>(xs[r], ths[r], is * kWScale, h, bins, A, B);
+        const int li = r * kThreads + tid;
+        s_g[swz(li)] = make_float2(-is * A, LOGSIG ? -(kLn10 * kInvW) * B : -(is * kInvW) * B);
+        s_lp[li] = (int16_t)(ps[r] - t.p0);
+      }
+    }
+  }
+  __syncthreads();
+  // ---- phase 2: 8 consecutive halos per thread; a population belongs to the thread that
+  // holds its FIRST halo in the tile
+  const int base = tid * kItems;
+  const int cnt = max(0, min(kItems, n - base));
+  float2 g[kItems];
+  int lp[kItems];
+  {
+    const float4* sg4 = reinterpret_cast<const float4*>(s_g);
+    const int sw = (tid >> 2) & 3;
+#pragma unroll
+    for (int k = 0; k < kItems / 2; ++k) {
+      const float4 v = sg4[4 * tid + (k ^ sw)];
+      g[2 * k] = make_float2(v.x, v.y);
+      g[2 * k + 1] = make_float2(v.z, v.w);
+    }
+    const uint4 l4 = reinterpret_cast<const uint4*>(s_lp)[tid];
+    const unsigned lw[4] = {l4.x, l4.y, l4.z, l4.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      lp[2 * k] = (int)(lw[k] & 0xFFFFu);
+      lp[2 * k + 1] = (int)(lw[k] >> 16);
+    }
+  }
+#pragma unroll
+  for (int j = 1; j < kItems; ++j) {  // past the tile end: same population, zero contribution
+    const bool in = j < cnt;
+    lp[j] = in ? lp[j] : lp[j - 1];
+    g[j].x = in ? g[j].x : 0.0f;
+    g[j].y = in ? g[j].y : 0.0f;
+  }
+  const int prevlp = (cnt > 0 && base > 0) ? (int)s_lp[base - 1] : -1;
+  const int nextlp = base + kItems < n ? (int)s_lp[base + kItems] : npops;
+  __syncthreads();  // contributions and ids are in registers: s_g, s_lp are reused
+  for (int k = tid; k < npops; k += kThreads) res[k] = make_float2(0.f, 0.f);  // no halos: 0
+  __syncthreads();
+  int c = lp[0];
+  float2 cur = g[0];
+  const bool headcont = cnt > 0 && c == prevlp;  // first segment continues an earlier thread's
+  bool inhead = true;
+  float2 hsum = make_float2(0.f, 0.f);
+  if (cnt > 0) {
+#pragma unroll
+    for (int j = 1; j < kItems; ++j) {
+      const bool brk = lp[j] != c;
+      const bool hb = brk && inhead && headcont;
+      if (brk && !hb) res[c] = cur;  // a whole segment inside this thread
+      hsum.x = hb ? cur.x : hsum.x;
+      hsum.y = hb ? cur.y : hsum.y;
+      inhead = inhead && !brk;
+      cur.x = brk ? g[j].x : cur.x + g[j].x;
+      cur.y = brk ? g[j].y : cur.y + g[j].y;
+      c = lp[j];
+    }
+  }
+  const bool contonly = cnt > 0 && inhead && headcont;  // every halo continues the head
+  if (contonly) hsum = cur;
+  s_head[tid] = hsum;
+  s_pass[tid] = contonly && nextlp == c;  // ... and it goes on into the next thread
+  __syncthreads();
+  if (cnt > 0 && !contonly) {  // this thread owns its tail segment (population c)
+    if (nextlp == c) {
+      for (int k = tid + 1; k < kThreads; ++k) {
+        const float2 hp = s_head[k];
+        cur.x += hp.x;
+        cur.y += hp.y;
+        if (!s_pass[k]) break;
+      }
+    }
+    res[c] = cur;
+  }
+  __syncthreads();
+  for (int k = tid; k < npops; k += kThreads) gout[k] = res[k];
 }
 
 // Measured on MI355X (1e7 params, 1.34e8 halos, internal order, with residuals): the
@@ -1943,12 +2214,20 @@ void smf_vjp(torch::Tensor x, c10::optional<torch::Tensor> pop, torch::Tensor th
   const Tile* tl = reinterpret_cast<const Tile*>(tiles.data_ptr<int64_t>()) + tile_begin;
   float2* gp = reinterpret_cast<float2*>(grad.data_ptr<float>());
   float2* pa = partials.numel() ? reinterpret_cast<float2*>(partials.data_ptr<float>()) : nullptr;
+  // the recurrence kernel needs uniform, unpadded bins (b.delta > 0) and population ids
+  const bool rec = MG_VJP_REC && b.delta > 0.0f && has_pop;
   if (ntiles > 0) {
     MG_DISPATCH_NB(nbp, {
-      if (log_sigma)
+      if (rec) {
+        if (log_sigma)
+          hipLaunchKernelGGL((smf_vjp_tiles_rec_kernel<NB, true>), dim3(ntiles), dim3(kThreads), 0, stream, xp, pp, tp, tl, h.data_ptr<float>(), b, gp, pa);
+        else
+          hipLaunchKernelGGL((smf_vjp_tiles_rec_kernel<NB, false>), dim3(ntiles), dim3(kThreads), 0, stream, xp, pp, tp, tl, h.data_ptr<float>(), b, gp, pa);
+      } else if (log_sigma) {
         hipLaunchKernelGGL((smf_vjp_tiles_kernel<NB, true>), dim3(ntiles), dim3(kThreads), 0, stream, xp, pp, tp, tl, h.data_ptr<float>(), b, gp, pa);
-      else
+      } else {
         hipLaunchKernelGGL((smf_vjp_tiles_kernel<NB, false>), dim3(ntiles), dim3(kThreads), 0, stream, xp, pp, tp, tl, h.data_ptr<float>(), b, gp, pa);
+      }
     });
   }
   const int64_t ng = giant.numel() / 3;
