@@ -35,7 +35,8 @@ void smf_forward_lanes(torch::Tensor xi, torch::Tensor slot_pop, torch::Tensor g
                        c10::optional<torch::Tensor> wave_start,
                        c10::optional<torch::Tensor> queues,
                        c10::optional<std::vector<torch::Tensor>> update,
-                       std::vector<double> update_scalars);
+                       std::vector<double> update_scalars,
+                       c10::optional<torch::Tensor> defer, int64_t fix_blocks);
 void smf_vjp_lanes(torch::Tensor slot_pop, torch::Tensor slot_part, torch::Tensor theta,
                    torch::Tensor h, torch::Tensor resid, int64_t s0, int64_t s1,
                    std::vector<double> scale, bool log_sigma, torch::Tensor grad,
@@ -131,7 +132,8 @@ PYBIND11_MODULE(_C, m) {
         pybind11::arg("nblocks"), pybind11::arg("rel_tail"), pybind11::arg("resid") = pybind11::none(),
         pybind11::arg("wave_order") = pybind11::none(), pybind11::arg("wave_start") = pybind11::none(),
         pybind11::arg("queues") = pybind11::none(), pybind11::arg("update") = pybind11::none(),
-        pybind11::arg("update_scalars") = std::vector<double>());
+        pybind11::arg("update_scalars") = std::vector<double>(),
+        pybind11::arg("defer") = pybind11::none(), pybind11::arg("fix_blocks") = 0);
   m.def("lpt_waves", &mg::lpt_waves);
   m.def("smf_vjp_lanes", &mg::smf_vjp_lanes);
   m.def("smf_vjp_adam_lanes", &mg::smf_vjp_adam_lanes);

@@ -129,6 +129,9 @@ __device__ __forceinline__ const float4* tail_tab_lane(const float4* tab) {
 #ifndef MG_FWD_TAB_FOLD
 #define MG_FWD_TAB_FOLD 1
 #endif
+#ifndef MG_FWD_TAB_BATCH
+#define MG_FWD_TAB_BATCH 1
+#endif
 template <int NB, bool LOGSIG, bool REL, int REPL = 0>
 __device__ __forceinline__ void halo_mass(float x, float2 th, const SmfBins& b,
                                           float (&acc)[NB + 1], int (&cnt)[NB + 1],
@@ -138,6 +141,32 @@ __device__ __forceinline__ void halo_mass(float x, float2 th, const SmfBins& b,
   constexpr bool kFold = REPL > 0 && MG_FWD_TAB_FOLD;
   const float ninv = -inv_sigma<LOGSIG>(th.y) * (kFold ? kWScale * kTailTabInvH : kWScale);
   const float mu = -(x + th.x) * ninv;  // = (x + a) * kWScale / sigma (x kTailTabInvH)
+  if constexpr (kFold && MG_FWD_TAB_BATCH > 1) {
+    // table reads of MG_FWD_TAB_BATCH edges issued before their cubics (fewer LDS waits)
+    constexpr int BT = MG_FWD_TAB_BATCH;
+#pragma unroll
+    for (int e0 = 0; e0 <= NB; e0 += BT) {
+      float4 c[BT];
+      float s[BT];
+#pragma unroll
+      for (int j = 0; j < BT; ++j) {
+        const int e = e0 + j;
+        if (e > NB) break;
+        const float t = __builtin_amdgcn_fmed3f(fmaf(b.edge[e], ninv, mu), -(float)(kTailTabN / 2),
+                                                (float)(kTailTabN / 2) - 1.0f / 4096);
+        c[j] = tb[cvt_flr_i32(t) * REPL];
+        s[j] = __builtin_amdgcn_fractf(t);
+        cnt[e] += __builtin_popcountll(__builtin_amdgcn_ballot_w64(t < 0.0f));
+      }
+#pragma unroll
+      for (int j = 0; j < BT; ++j) {
+        const int e = e0 + j;
+        if (e > NB) break;
+        acc[e] += fma_scalar(fma_scalar(fma_scalar(c[j].w, s[j], c[j].z), s[j], c[j].y), s[j], c[j].x);
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int e = 0; e <= NB; ++e) {
     const float n = fmaf(b.edge[e], ninv, mu);
@@ -1291,6 +1320,9 @@ __global__ __launch_bounds__(kThreads, MG_VJP_REC_MINWAVES) void smf_vjp_tiles_r
 #ifndef MG_LANES_EP
 #define MG_LANES_EP 1
 #endif
+#ifndef MG_LANES_DEFER
+#define MG_LANES_DEFER 1  // residual forwards defer groups outside the EM range (LMODE 1)
+#endif
 
 // Packed two-halo path: 10% fewer VALU cycles per halo pair, but it needs 108 VGPRs
 // (4 waves/SIMD) to avoid spills; measured on MI355X it ties the scalar path (690 vs
@@ -1418,15 +1450,29 @@ __device__ __forceinline__ void lds_stage_block(const float* src, float* dst, in
                     std::make_integer_sequence<int, NR % 4>{});
 }
 
-template <int NB, bool LOGSIG, bool REL, bool RESID, bool UPD = false>
+// LMODE (Euler-Maclaurin residual forwards, MG_LANES_DEFER): 0 = plain; 1 = DEFER: a group
+// outside the EM range is not evaluated here but appended to the device list `defer`
+// ([count, done ticket, group ids...]) -- the kernel then carries no per-edge fallback code
+// (which cost ~3.5% of the headline step in registers although the headline data never
+// takes it: profiles/em_forward/, 2276-2291 vs 2204-2210 steps/s); 2 = LIST: the fix-up
+// launch that follows, over the listed groups only (EM + per-edge fallback, residuals and
+// its own slab rows), whose last workgroup resets the list for the next launch.
+template <int NB, bool LOGSIG, bool REL, bool RESID, bool UPD = false, int LMODE = 0>
 __global__ __launch_bounds__(kThreads, MG_LANES_MINWAVES) void smf_fwd_lanes_kernel(
     const float* __restrict__ xi, const int32_t* __restrict__ slot_pop,
     const int64_t* __restrict__ group_base, const int32_t* __restrict__ group_len,
     const int32_t* __restrict__ fwd_order, const float2* __restrict__ theta, int64_t g0,
     int64_t g1, SmfBins bins, float* __restrict__ slab, float* __restrict__ resid,
     const int32_t* __restrict__ wave_start, int* __restrict__ queues, int nq,
-    LanesUpdate upd = LanesUpdate{}) {
+    LanesUpdate upd = LanesUpdate{}, int* __restrict__ defer = nullptr) {
   static_assert(!UPD || RESID, "the pipelined update reads the residuals it overwrites");
+  static_assert(LMODE == 0 || (RESID && MG_FWD_EM && MG_LANES_EP && !REL), "deferral: EM residual forwards");
+  static_assert(LMODE != 2 || !UPD, "the fix-up launch evaluates updated groups");
+  if constexpr (LMODE == 2) {  // the listed groups, grid-strided
+    fwd_order = defer + 2;
+    g0 = 0;
+    g1 = __builtin_amdgcn_readfirstlane(__hip_atomic_load(defer, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  }
   // signed-tail table (absolute contract): 16 replicas (conflict-free reads), 8 next to
   // the pipelined update's staging buffer (LDS budget of 4 workgroups per CU)
   constexpr int kRepl =
@@ -1685,6 +1731,12 @@ __global__ __launch_bounds__(kThreads, MG_LANES_MINWAVES) void smf_fwd_lanes_ker
 #endif
     // the next kLanesUnroll loads are in flight while the current halos are computed;
     // past-the-end halos are the sentinel (exact zero contribution)
+    if constexpr (LMODE == 1) {
+      if (!em && lane == 0) {  // outside the EM range: the fix-up launch evaluates it
+        const int slot = atomicAdd(defer, 1);
+        defer[2 + slot] = (int)gc;
+      }
+    } else
 #ifdef MG_FWD_EM_ONLY
     if (!kEm)
 #else
@@ -1730,7 +1782,7 @@ __global__ __launch_bounds__(kThreads, MG_LANES_MINWAVES) void smf_fwd_lanes_ker
 #endif
     if constexpr (!UPD)
       if (kn < g1) load_group(kn, c_next);
-    if constexpr (RESID) {  // group-major [g][2 (NB+1)][64]: one contiguous block per group
+    if (RESID && (LMODE != 1 || em)) {  // group-major [g][2 (NB+1)][64]: one block per group
 #if MG_LANES_BUF
       const __amdgpu_buffer_rsrc_t rr = buf_rsrc(resid + gc * (2 * (NB + 1) * kWave));
 #else
@@ -1802,6 +1854,14 @@ __global__ __launch_bounds__(kThreads, MG_LANES_MINWAVES) void smf_fwd_lanes_ker
   if (threadIdx.x == 0) {
 #pragma unroll
     for (int k = 0; k < NB; ++k) slab[(int64_t)blockIdx.x * NB + k] = acc[k];
+    if constexpr (LMODE == 2) {
+      // every workgroup read the count at its start; the last one to finish resets the
+      // list for the next step's launch (self-resetting: graph-replay safe)
+      if (atomicAdd(defer + 1, 1) == (int)gridDim.x - 1) {
+        __hip_atomic_store(defer, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(defer + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
   }
 }
 
@@ -2367,7 +2427,8 @@ void smf_forward_lanes(torch::Tensor xi, torch::Tensor slot_pop, torch::Tensor g
                        c10::optional<torch::Tensor> wave_start,
                        c10::optional<torch::Tensor> queues,
                        c10::optional<std::vector<torch::Tensor>> update,
-                       std::vector<double> update_scalars) {
+                       std::vector<double> update_scalars,
+                       c10::optional<torch::Tensor> defer, int64_t fix_blocks) {
   check_dev(xi, "xi", at::kFloat);
   check_dev(slot_pop, "slot_pop", at::kInt);
   check_dev(group_base, "group_base", at::kLong);
@@ -2416,6 +2477,39 @@ void smf_forward_lanes(torch::Tensor xi, torch::Tensor slot_pop, torch::Tensor g
   const SmfBins b = make_bins(edges, scale, nbp);
   auto stream = at::hip::getCurrentHIPStream();
   const float2* tp = reinterpret_cast<const float2*>(theta.data_ptr<float>());
+  // Residual forwards with a deferral list (see LMODE): the main launch defers groups outside
+  // the Euler-Maclaurin range, then a fix-up launch of fix_blocks workgroups evaluates them
+  // into slab rows [nblocks, nblocks + fix_blocks) (zero rows when nothing was deferred).
+  // Without uniform bins every group would be deferred: the main launch keeps its own
+  // per-edge path and the fix-up rows are zeroed.
+  int* dp = nullptr;
+  if (defer.has_value() && defer->defined()) {
+    TORCH_CHECK(has_resid, "the deferral list is for residual forwards");
+    check_dev(*defer, "defer", at::kInt);
+    TORCH_CHECK(defer->numel() >= 2 + ng, "defer: [count, ticket, one slot per group]");
+    TORCH_CHECK(fix_blocks >= 1 && fix_blocks <= 65535, "bad fix-up block count");
+    TORCH_CHECK(slab.numel() >= (nblocks + fix_blocks) * nbp, "slab too small for the fix-up rows");
+    dp = defer->data_ptr<int>();
+  }
+  const bool lmode = dp != nullptr && MG_FWD_EM && MG_LANES_EP && MG_LANES_DEFER && !rel_tail &&
+                     b.delta > 0.0f;
+  auto fixup = [&]() {
+    if (dp == nullptr) return;
+    float* fs = slab.data_ptr<float>() + nblocks * nbp;
+    if (!lmode) {
+      hipMemsetAsync(fs, 0, sizeof(float) * fix_blocks * nbp, stream);
+      return;
+    }
+    MG_DISPATCH_NB(nbp, {
+      with_bool(log_sigma, [&](auto LS) {
+        hipLaunchKernelGGL((smf_fwd_lanes_kernel<NB, decltype(LS)::value, false, true, false, 2>),
+                           dim3(fix_blocks), dim3(kThreads), 0, stream, xi.data_ptr<float>(),
+                           slot_pop.data_ptr<int32_t>(), group_base.data_ptr<int64_t>(),
+                           group_len.data_ptr<int32_t>(), fwd_order.data_ptr<int32_t>(), tp,
+                           (int64_t)0, (int64_t)0, b, fs, rp, nullptr, nullptr, 0, LanesUpdate{}, dp);
+      });
+    });
+  };
   if (update.has_value()) {
     // pipelined update: tensors [h, m, v, step(int32[2]), traj (or empty)]; scalars
     // [unit_offset, host_step, lr, b1, b2, eps, traj_stride]
@@ -2448,27 +2542,49 @@ void smf_forward_lanes(torch::Tensor xi, torch::Tensor slot_pop, torch::Tensor g
                 "bad unit offset");
     u.step = U[3].data_ptr<int>();
     MG_DISPATCH_NB(nbp, {
-      with_bool(log_sigma, [&](auto LS) { with_bool(rel_tail, [&](auto RT) {
-        hipLaunchKernelGGL((smf_fwd_lanes_kernel<NB, decltype(LS)::value, decltype(RT)::value, true, true>),
-                           dim3(nblocks), dim3(kThreads), 0, stream, xi.data_ptr<float>(),
-                           slot_pop.data_ptr<int32_t>(), group_base.data_ptr<int64_t>(),
-                           group_len.data_ptr<int32_t>(), order, tp, g0, g1, b,
-                           slab.data_ptr<float>(), rp, ws, qp, nq, u);
-      }); });
+      with_bool(log_sigma, [&](auto LS) {
+        if (lmode) {
+          hipLaunchKernelGGL((smf_fwd_lanes_kernel<NB, decltype(LS)::value, false, true, true, MG_LANES_DEFER>),
+                             dim3(nblocks), dim3(kThreads), 0, stream, xi.data_ptr<float>(),
+                             slot_pop.data_ptr<int32_t>(), group_base.data_ptr<int64_t>(),
+                             group_len.data_ptr<int32_t>(), order, tp, g0, g1, b,
+                             slab.data_ptr<float>(), rp, ws, qp, nq, u, dp);
+        } else {
+          with_bool(rel_tail, [&](auto RT) {
+            hipLaunchKernelGGL((smf_fwd_lanes_kernel<NB, decltype(LS)::value, decltype(RT)::value, true, true>),
+                               dim3(nblocks), dim3(kThreads), 0, stream, xi.data_ptr<float>(),
+                               slot_pop.data_ptr<int32_t>(), group_base.data_ptr<int64_t>(),
+                               group_len.data_ptr<int32_t>(), order, tp, g0, g1, b,
+                               slab.data_ptr<float>(), rp, ws, qp, nq, u);
+          });
+        }
+      });
     });
+    fixup();  // after the update: the listed groups are evaluated at their new parameters
     if (u.host_step < 0 && !defer_advance)
       hipLaunchKernelGGL(smf_advance_step_kernel, dim3(1), dim3(1), 0, stream, U[3].data_ptr<int>());
     return;
   }
   MG_DISPATCH_NB(nbp, {
-    with_bool(log_sigma, [&](auto LS) { with_bool(rel_tail, [&](auto RT) { with_bool(has_resid, [&](auto RS) {
-      hipLaunchKernelGGL((smf_fwd_lanes_kernel<NB, decltype(LS)::value, decltype(RT)::value, decltype(RS)::value>),
-                         dim3(nblocks), dim3(kThreads), 0, stream, xi.data_ptr<float>(),
-                         slot_pop.data_ptr<int32_t>(), group_base.data_ptr<int64_t>(),
-                         group_len.data_ptr<int32_t>(), order, tp, g0, g1, b,
-                         slab.data_ptr<float>(), rp, ws, qp, nq);
-    }); }); });
+    with_bool(log_sigma, [&](auto LS) {
+      if (lmode) {
+        hipLaunchKernelGGL((smf_fwd_lanes_kernel<NB, decltype(LS)::value, false, true, false, MG_LANES_DEFER>),
+                           dim3(nblocks), dim3(kThreads), 0, stream, xi.data_ptr<float>(),
+                           slot_pop.data_ptr<int32_t>(), group_base.data_ptr<int64_t>(),
+                           group_len.data_ptr<int32_t>(), order, tp, g0, g1, b,
+                           slab.data_ptr<float>(), rp, ws, qp, nq, LanesUpdate{}, dp);
+      } else {
+        with_bool(rel_tail, [&](auto RT) { with_bool(has_resid, [&](auto RS) {
+          hipLaunchKernelGGL((smf_fwd_lanes_kernel<NB, decltype(LS)::value, decltype(RT)::value, decltype(RS)::value>),
+                             dim3(nblocks), dim3(kThreads), 0, stream, xi.data_ptr<float>(),
+                             slot_pop.data_ptr<int32_t>(), group_base.data_ptr<int64_t>(),
+                             group_len.data_ptr<int32_t>(), order, tp, g0, g1, b,
+                             slab.data_ptr<float>(), rp, ws, qp, nq);
+        }); });
+      }
+    });
   });
+  fixup();
 }
 
 // Residual VJP over slots [s0, s1) plus the fixed-order finalize of split populations

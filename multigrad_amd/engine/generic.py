@@ -545,19 +545,24 @@ class GraphAdamEngine:
             self.graph.replay()
         cur.wait_stream(self._rs)
 
-    _TUNE = 3  # steps timed per mode by the auto policy
+    _TUNE = 6       # steps per timed window of the auto policy
+    _TUNE_WARM = 3  # eager steps before the first window (lazy init, first launches, clocks)
 
     def _tuned_step(self, key):
-        """Auto policy (``graph=None``): the first steps run eagerly, the next ones from
-        the captured graph; each window of steps is timed as a whole (no synchronisation
-        inside it, so eager launches overlap the GPU as in steady state) and the faster
-        mode is kept -- a collective decision.  Measured on one MI355X
-        (profiles/generic_engine.md): replay wins when the step is launch bound (1.4-1.8x
-        on a 1e4-parameter torch model) and loses ~10% when it is GPU bound."""
+        """Auto policy (``graph=None``): after ``_TUNE_WARM`` eager steps, a window of
+        ``_TUNE`` eager steps, then the capture and one untimed replay, then a window of
+        ``_TUNE`` replays; each window is timed as a whole (no synchronisation inside it,
+        so eager launches overlap the GPU as in steady state).  Replay is kept only if it
+        beats eager by 3% -- a collective decision -- and then simply continues, so a
+        replay never follows eager steps of the tuning (such a default-stream replay after
+        eager work and a host synchronisation computed wrong sums on this runtime, see
+        _replay).  Measured on one MI355X (profiles/generic_engine.md): replay wins only
+        when the step is launch bound and loses when it is GPU bound."""
         import time
-        k, T = self.step_host, self._TUNE
-        mode = "eager" if k < T else "graph"
-        if mode == "graph" and self.graph is None:
+        k, T, W = self.step_host, self._TUNE, self._TUNE_WARM
+        # phase: -1 warm-up, 0 eager window, 1 first (untimed) replay, 2 replay window
+        ph = -1 if k < W else 0 if k < W + T else 1 if k == W + T else 2
+        if ph >= 1 and self.graph is None:
             self.step_dev[0] = k   # eager steps keep the count on the host
             try:
                 self.graph = self._capture()
@@ -569,19 +574,19 @@ class GraphAdamEngine:
                 self.fallback_reason = f"capture failed: {type(exc).__name__}: {exc}"
                 self._body(k, key)
                 return
-        if k in (0, T):
+        if k in (W, W + T + 1):
             torch.cuda.synchronize()
             self._t0 = time.perf_counter()
-        if mode == "graph":
+        if ph >= 1:
             self._replay(key)
         else:
             self._body(k, key)
-        if k in (T - 1, 2 * T - 1):
+        if k in (W + T - 1, W + 2 * T):
             torch.cuda.synchronize()
-            self._times[mode] = time.perf_counter() - self._t0
-        if k == 2 * T - 1:
-            te, tg = self._times["eager"] / T, self._times["graph"] / T
-            keep = 1 if tg < te else 0
+            self._times[ph] = time.perf_counter() - self._t0
+        if k == W + 2 * T:
+            te, tg = self._times[0] / T, self._times[2] / T
+            keep = 1 if tg < 0.97 * te else 0
             if self.size > 1:
                 keep = int(all(self.comm.allgather(keep)))
             self.tuning = {"eager_s": te, "graph_s": tg, "graph": bool(keep)}
@@ -597,7 +602,7 @@ class GraphAdamEngine:
             raise RuntimeError("more steps than the trajectory buffer was sized for")
         key = self._step_key()
         if self.use_graph and self.graph_req is None and self.tuning is None and \
-                self.nsteps > 2 * self._TUNE:
+                self.nsteps > 3 * self._TUNE + self._TUNE_WARM:
             self._tuned_step(key)
             self.step_host += 1
             if self.history.mode != "full" and self.traj_loc is None:

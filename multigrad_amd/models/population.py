@@ -259,8 +259,8 @@ class PopulationSMFModel(OnePointModel):
         if self.shard.device.type != "cuda":
             return 1
         h0, h1 = self.shard.halo_range(chunk)
-        return self.shard.fwd_blocks(max(h1 - h0, 1), self.bins.nb, True, self.bins.rel_tail,
-                                     chunk)
+        return self.shard.fwd_rows(max(h1 - h0, 1), self.bins.nb, True, self.bins.rel_tail,
+                                   chunk, resid=True)
 
     def engine_forward_chunk(self, theta, slab, chunk=None) -> int:
         # the engine always runs the VJP of a chunk after this forward at the same theta,

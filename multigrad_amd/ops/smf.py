@@ -307,6 +307,24 @@ class PopulationShard:
             self.resid = torch.empty(shape, dtype=torch.float32, device=self.device)
         return self.resid
 
+    def defer_buffer(self) -> torch.Tensor:
+        """Device list of the residual lanes forwards ([count, ticket, one slot per group]):
+        groups outside the Euler-Maclaurin range are deferred by the main launch to a
+        fix-up launch of LANES_FIX_BLOCKS workgroups (csrc/smf.hip, LMODE).  Both counters
+        are left at 0 by the fix-up launch itself."""
+        if getattr(self, "_defer", None) is None or self._defer.numel() < 2 + self.ngroups:
+            self._defer = torch.zeros(2 + self.ngroups, dtype=torch.int32, device=self.device)
+        return self._defer
+
+    def fwd_rows(self, nhalos: int, nbins: int = 10, log_sigma: bool = True,
+                 rel_tail: bool = False, chunk: Optional[int] = None, resid: bool = True) -> int:
+        """Slab rows a forward over ``chunk`` writes: the forward grid (:meth:`fwd_blocks`)
+        plus, for residual forwards of the lanes layout, the fix-up launch's rows."""
+        n = self.fwd_blocks(nhalos, nbins, log_sigma, rel_tail, chunk)
+        if self.device.type == "cuda" and self.layout == "lanes" and resid:
+            n += LANES_FIX_BLOCKS
+        return n
+
     @property
     def vjp_recompute(self) -> bool:
         """Lanes layout with local slot order: the VJP re-evaluates the halos (no
@@ -358,6 +376,9 @@ class PopulationShard:
 
 
 _GRID_CACHE: dict = {}
+# workgroups of the fix-up launch that evaluates the groups a residual lanes forward deferred
+# (outside the Euler-Maclaurin range; none in the headline data): one wave of 64 groups each
+LANES_FIX_BLOCKS = 64
 
 
 def _sort_by_population(pop_cpu: torch.Tensor, npop: int):
@@ -460,9 +481,12 @@ def smf_forward_slab(theta: torch.Tensor, shard: PopulationShard, bins: SmfBins,
         ext().smf_forward_lanes(shard.xi, shard.slot_index(order), shard.group_base,
                                 shard.group_len, shard.fwd_order, theta, list(bins.edges),
                                 list(bins.scale), bool(log_sigma), g0, g1, slab, nblk,
-                                bins.rel_tail, rbuf, w_order, w_start, queues, upd, usc)
+                                bins.rel_tail, rbuf, w_order, w_start, queues, upd, usc,
+                                shard.defer_buffer() if resid else None,
+                                LANES_FIX_BLOCKS if resid else 0)
         if resid:
             shard.resid_epoch += 1
+            return nblk + LANES_FIX_BLOCKS
         return nblk
     ext().smf_forward(shard.x, shard.pop, theta, list(bins.edges), list(bins.scale),
                       bool(log_sigma), h0, h1, slab, nblk, bins.rel_tail)
@@ -525,7 +549,7 @@ def smf_forward_into(theta: torch.Tensor, shard: PopulationShard, bins: SmfBins,
     """Partial sumstats of the shard (or one population chunk) into ``out[:nbp]``."""
     if slab is None:
         h0, h1 = shard.halo_range(chunk)
-        nblk = shard.fwd_blocks(max(h1 - h0, 1), bins.nb, log_sigma, bins.rel_tail, chunk)
+        nblk = shard.fwd_rows(max(h1 - h0, 1), bins.nb, log_sigma, bins.rel_tail, chunk, resid)
         slab = torch.empty(nblk * bins.nbp, dtype=torch.float32, device=theta.device)
     nrows = smf_forward_slab(theta, shard, bins, log_sigma, slab, chunk, resid, order)
     return smf_slab_reduce(slab, nrows, bins, out)
@@ -582,7 +606,7 @@ def smf_vjp_into(theta: torch.Tensor, shard: PopulationShard, bins: SmfBins, log
         return grad
     if shard.layout == "lanes":
         if not residuals_ready or shard.resid is None:
-            nblk = shard.fwd_blocks(1, bins.nb, log_sigma, bins.rel_tail, chunk)
+            nblk = shard.fwd_rows(1, bins.nb, log_sigma, bins.rel_tail, chunk, resid=True)
             slab = torch.empty(nblk * bins.nbp, dtype=torch.float32, device=theta.device)
             smf_forward_slab(theta, shard, bins, log_sigma, slab, chunk, resid=True, order=order)
         g0, g1 = shard.group_range(chunk)

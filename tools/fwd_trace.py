@@ -28,7 +28,7 @@ def main():
     shard, bins = data["shard"], data["bins"]
     th = data["guess"].reshape(-1, 2)[shard.perm].reshape(-1).contiguous()
     out = torch.zeros(bins.nbp, device=dev)
-    nblk = shard.fwd_blocks(shard.n, bins.nb, True, bins.rel_tail)
+    nblk = shard.fwd_rows(shard.n, bins.nb, True, bins.rel_tail, resid=True)
     slab = torch.zeros(nblk * bins.nbp, device=dev)
     for _ in range(3):
         S.smf_forward_into(th, shard, bins, True, out, slab=slab, resid=True, order="internal")

@@ -39,7 +39,7 @@ def main():
     shard, bins = data["shard"], data["bins"]
     th = data["guess"]
     out = torch.zeros(bins.nbp, device=dev)
-    nblk = shard.fwd_blocks(shard.n, bins.nb, True, bins.rel_tail)
+    nblk = shard.fwd_rows(shard.n, bins.nb, True, bins.rel_tail, resid=True)
     slab = torch.zeros(nblk * bins.nbp, device=dev)
     h = torch.zeros(bins.nbp + 1, device=dev)
     loss = torch.zeros(1, device=dev)
