@@ -366,13 +366,20 @@ __global__ void logmse_loss_kernel(const float* __restrict__ S, const float* __r
 //   -> cross-rank sum through the one-shot peer-memory exchange      [xgmi.h, size > 1]
 //   -> log-MSE loss and edge weights h (padded edges zeroed)         [logmse_loss_kernel]
 // Replaces three launches and a memset per step (~14 us on an 8-GPU owner shard).
+// One workgroup of MG_EPI_THREADS (1024 threads, one round of slab-row loads per thread,
+// measured 14.6 vs 8.0 us per launch at the headline: the wider block reduction and its
+// barriers cost more than the load round trips they save)
+#ifndef MG_EPI_THREADS
+#define MG_EPI_THREADS 256
+#endif
+constexpr int kEpiThreads = MG_EPI_THREADS;
 template <int NB>
-__global__ __launch_bounds__(kThreads) void smf_epilogue_kernel(
+__global__ __launch_bounds__(kEpiThreads) void smf_epilogue_kernel(
     const float* __restrict__ slab, int nrows, int nb, SmfBins bins, XgmiPeers peers, int rank,
     int size, unsigned* seq, int* err, long long ticks, const float* __restrict__ target,
     float eps, float* __restrict__ S_out, float* __restrict__ loss, float* __restrict__ h,
     int* advance) {
-  __shared__ double scratch[NB * (kThreads / kWave)];
+  __shared__ double scratch[NB * (kEpiThreads / kWave)];
   __shared__ float Sv[kXMaxFloats];
   __shared__ float g[kMaxBins];
   __shared__ float d2[kMaxBins];
@@ -382,18 +389,18 @@ __global__ __launch_bounds__(kThreads) void smf_epilogue_kernel(
   // rows four at a time with every load issued before the first add (one memory round trip
   // per four rows instead of one per row); the per-thread order of the sums is unchanged
   int r = threadIdx.x;
-  for (; r + 3 * kThreads < nrows; r += 4 * kThreads) {
+  for (; r + 3 * kEpiThreads < nrows; r += 4 * kEpiThreads) {
     float a[4][NB];
 #pragma unroll
     for (int u = 0; u < 4; ++u)
 #pragma unroll
-      for (int k = 0; k < NB; ++k) a[u][k] = slab[(int64_t)(r + u * kThreads) * NB + k];
+      for (int k = 0; k < NB; ++k) a[u][k] = slab[(int64_t)(r + u * kEpiThreads) * NB + k];
 #pragma unroll
     for (int u = 0; u < 4; ++u)
 #pragma unroll
       for (int k = 0; k < NB; ++k) v[k] += (double)a[u][k];
   }
-  for (; r < nrows; r += kThreads) {
+  for (; r < nrows; r += kEpiThreads) {
 #pragma unroll
     for (int k = 0; k < NB; ++k) v[k] += (double)slab[(int64_t)r * NB + k];
   }
@@ -2241,7 +2248,7 @@ void smf_epilogue(torch::Tensor slab, int64_t nrows, std::vector<double> edges,
   auto stream = at::hip::getCurrentHIPStream();
   const long long ticks = (long long)(timeout_s * 1e8);
   MG_DISPATCH_NB(nbp, {
-    hipLaunchKernelGGL((smf_epilogue_kernel<NB>), dim3(1), dim3(kThreads), 0, stream,
+    hipLaunchKernelGGL((smf_epilogue_kernel<NB>), dim3(1), dim3(kEpiThreads), 0, stream,
                        slab.data_ptr<float>(), (int)nrows, nb, b, p, (int)rank, size, sq, er, ticks,
                        target.data_ptr<float>(), (float)eps, S.data_ptr<float>(),
                        loss.data_ptr<float>(), h.data_ptr<float>(), adv);

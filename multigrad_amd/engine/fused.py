@@ -171,9 +171,10 @@ class FusedAdamEngine:
 
         Hashed placement on several GPUs with the two-shot exchange and no explicit chunk
         count: the two-chunk layout (whose exchange may overlap the VJP on a side stream) is
-        timed against one chunk (one cross-rank rendezvous per step instead of two), and
-        the faster is kept -- both by the same setup-time measurement as the rest of the
-        schedule (:meth:`_autotune`)."""
+        timed against one chunk (one cross-rank rendezvous per step instead of two) and,
+        when the overlapped two-chunk schedule won, against four overlapped chunks
+        (``MULTIGRAD_MAX_CHUNKS``, default 4); the fastest is kept -- all by the same
+        setup-time measurement as the rest of the schedule (:meth:`_autotune`)."""
         kw = dict(param_bounds=param_bounds, learning_rate=learning_rate, b1=b1, b2=b2,
                   eps=eps, history=history, legacy_bounds_jacobian=legacy_bounds_jacobian)
         self._chunks_override = None
@@ -196,20 +197,40 @@ class FusedAdamEngine:
         self._autotune(cands, min_window_s=1e-3 * float(
             os.environ.get("MULTIGRAD_AUTOTUNE_WINDOW_MS", "30")))
         t1 = min(c["ms"] for c in self.tuning["candidates"])
+        tun1 = self.tuning
         chunk_times = {"1": t1, "2": t2}
-        if t1 <= t2:
-            self.tuning["chunks"] = dict(chunk_times, chosen=1)
-            return self
-        self._chunks_override = 2
-        self._skip_autotune = True
-        try:
-            self._setup(guess, nsteps, **kw)
-        finally:
-            self._skip_autotune = skip
-        for k, v in tun["chosen"].items():
-            setattr(self, k, v)
-        self.graph = None
-        self.tuning = dict(tun, chunks=dict(chunk_times, chosen=2))
+        tuned = {1: tun1, 2: tun}
+        current = 1
+        nmax = int(os.environ.get("MULTIGRAD_MAX_CHUNKS", "4"))
+        if nmax >= 4 and t2 < t1:
+            # the overlapped schedule won with two chunks: four give the exchange of each
+            # chunk a shorter wait behind its VJP and the next forward a shorter wait behind
+            # its exchange (one more cross-rank rendezvous per extra chunk)
+            self._chunks_override = 4
+            self._skip_autotune = True
+            try:
+                self._setup(guess, nsteps, **kw)
+            finally:
+                self._skip_autotune = skip
+            if self.C == 4 and self.comm_stream is not None:
+                self._autotune([{"ts_side": True, "rccl_exchange": False}],
+                               min_window_s=1e-3 * float(
+                                   os.environ.get("MULTIGRAD_AUTOTUNE_WINDOW_MS", "30")))
+                chunk_times["4"] = min(c["ms"] for c in self.tuning["candidates"])
+                tuned[4] = self.tuning
+                current = 4
+        best = min(tuned, key=lambda c: chunk_times[str(c)])
+        if best != current:
+            self._chunks_override = best
+            self._skip_autotune = True
+            try:
+                self._setup(guess, nsteps, **kw)
+            finally:
+                self._skip_autotune = skip
+            for k, v in tuned[best]["chosen"].items():
+                setattr(self, k, v)
+            self.graph = None
+        self.tuning = dict(tuned[best], chunks=dict(chunk_times, chosen=best))
         return self
 
     def _setup(self, guess, nsteps: int, param_bounds=None, learning_rate: float = 0.01,

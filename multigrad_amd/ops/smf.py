@@ -378,7 +378,7 @@ class PopulationShard:
 _GRID_CACHE: dict = {}
 # workgroups of the fix-up launch that evaluates the groups a residual lanes forward deferred
 # (outside the Euler-Maclaurin range; none in the headline data): one wave of 64 groups each
-LANES_FIX_BLOCKS = 64
+LANES_FIX_BLOCKS = int(os.environ.get("MULTIGRAD_FIX_BLOCKS", "64"))
 
 
 def _sort_by_population(pop_cpu: torch.Tensor, npop: int):
