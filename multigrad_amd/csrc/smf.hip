@@ -1864,7 +1864,7 @@ __global__ __launch_bounds__(kThreads, MG_LANES_MINWAVES) void smf_fwd_lanes_ker
     if constexpr (LMODE == 2) {
       // every workgroup read the count at its start; the last one to finish resets the
       // list for the next step's launch (self-resetting: graph-replay safe)
-      if (atomicAdd(defer + 1, 1) == (int)gridDim.x - 1) {
+      if (gridDim.x == 1 || atomicAdd(defer + 1, 1) == (int)gridDim.x - 1) {
         __hip_atomic_store(defer, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(defer + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }

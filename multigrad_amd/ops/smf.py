@@ -377,8 +377,10 @@ class PopulationShard:
 
 _GRID_CACHE: dict = {}
 # workgroups of the fix-up launch that evaluates the groups a residual lanes forward deferred
-# (outside the Euler-Maclaurin range; none in the headline data): one wave of 64 groups each
-LANES_FIX_BLOCKS = int(os.environ.get("MULTIGRAD_FIX_BLOCKS", "64"))
+# (outside the Euler-Maclaurin range; none in the headline data).  An empty fix-up launch of
+# 64 workgroups measured 16.5 us, of 1 workgroup 7.4 us (the count read and the reset are
+# memory round trips; the 64 tickets serialise): 8 keeps 32 waves for data that defers
+LANES_FIX_BLOCKS = int(os.environ.get("MULTIGRAD_FIX_BLOCKS", "8"))
 
 
 def _sort_by_population(pop_cpu: torch.Tensor, npop: int):
