@@ -3,7 +3,7 @@
 # profile of the bench, and the generic-engine benchmarks with the reworked auto policy.
 set -u
 R=${GRAFT_REPO_ROOT:-$(pwd)}
-O=$R/gpurun_out/s3b
+O=$R/gpurun_out/${S3B_OUT:-s3b}
 mkdir -p "$O"
 cd "$R"
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
@@ -23,7 +23,3 @@ for m in plain randkey group; do
     --model $m --repeats 5 >> "$O/generic.log" 2>&1 || { echo "generic $m failed"; exit 1; }
 done
 grep speedup "$O/generic.log" | cut -c1-200
-if [ -f variants/epi256/_C.so ]; then
-  bash tools/ab_script_so.sh epi256 bench.py --steps 50 --warmup 5 --no-count-launches > "$O/ab_epi.log" 2>&1
-  cut -c1-160 "$O/ab_epi.log"
-fi
