@@ -25,7 +25,7 @@ void smf_vjp(torch::Tensor x, c10::optional<torch::Tensor> pop, torch::Tensor th
 int64_t smf_fwd_lanes_max_blocks(int64_t nb, bool log_sigma, bool rel_tail, bool resid);
 void smf_lanes_pack(torch::Tensor xs, torch::Tensor slot_src, torch::Tensor slot_len,
                     torch::Tensor group_base, torch::Tensor group_len, torch::Tensor xi);
-void smf_forward_lanes(torch::Tensor xi, torch::Tensor slot_pop, torch::Tensor group_base,
+int64_t smf_forward_lanes(torch::Tensor xi, torch::Tensor slot_pop, torch::Tensor group_base,
                        torch::Tensor group_len, torch::Tensor fwd_order, torch::Tensor theta,
                        std::vector<double> edges,
                        std::vector<double> scale, bool log_sigma, int64_t g0, int64_t g1,
@@ -36,7 +36,9 @@ void smf_forward_lanes(torch::Tensor xi, torch::Tensor slot_pop, torch::Tensor g
                        c10::optional<torch::Tensor> queues,
                        c10::optional<std::vector<torch::Tensor>> update,
                        std::vector<double> update_scalars,
-                       c10::optional<torch::Tensor> defer, int64_t fix_blocks);
+                       c10::optional<torch::Tensor> defer, int64_t fix_blocks,
+                       std::vector<torch::Tensor> epi_tensors, std::vector<double> epi_scalars,
+                       std::vector<int64_t> epi_peers);
 void smf_vjp_lanes(torch::Tensor slot_pop, torch::Tensor slot_part, torch::Tensor theta,
                    torch::Tensor h, torch::Tensor resid, int64_t s0, int64_t s1,
                    std::vector<double> scale, bool log_sigma, torch::Tensor grad,
@@ -133,7 +135,10 @@ PYBIND11_MODULE(_C, m) {
         pybind11::arg("wave_order") = pybind11::none(), pybind11::arg("wave_start") = pybind11::none(),
         pybind11::arg("queues") = pybind11::none(), pybind11::arg("update") = pybind11::none(),
         pybind11::arg("update_scalars") = std::vector<double>(),
-        pybind11::arg("defer") = pybind11::none(), pybind11::arg("fix_blocks") = 0);
+        pybind11::arg("defer") = pybind11::none(), pybind11::arg("fix_blocks") = 0,
+        pybind11::arg("epi_tensors") = std::vector<torch::Tensor>(),
+        pybind11::arg("epi_scalars") = std::vector<double>(),
+        pybind11::arg("epi_peers") = std::vector<int64_t>());
   m.def("lpt_waves", &mg::lpt_waves);
   m.def("smf_vjp_lanes", &mg::smf_vjp_lanes);
   m.def("smf_vjp_adam_lanes", &mg::smf_vjp_adam_lanes);

@@ -373,34 +373,51 @@ __global__ void logmse_loss_kernel(const float* __restrict__ S, const float* __r
 #define MG_EPI_THREADS 256
 #endif
 constexpr int kEpiThreads = MG_EPI_THREADS;
-template <int NB>
-__global__ __launch_bounds__(kEpiThreads) void smf_epilogue_kernel(
-    const float* __restrict__ slab, int nrows, int nb, SmfBins bins, XgmiPeers peers, int rank,
-    int size, unsigned* seq, int* err, long long ticks, const float* __restrict__ target,
-    float eps, float* __restrict__ S_out, float* __restrict__ loss, float* __restrict__ h,
-    int* advance) {
-  __shared__ double scratch[NB * (kEpiThreads / kWave)];
+
+// Arguments of the sumstat epilogue (see smf_epilogue_kernel); `on` = 0: none.
+struct EpiArgs {
+  const float* slab;
+  int nrows, nb, rank, size, on;
+  XgmiPeers peers;
+  unsigned* seq;
+  int* err;
+  long long ticks;
+  const float* target;
+  float eps;
+  float* S_out;
+  float* loss;
+  float* h;
+  int* advance;
+};
+
+// The epilogue as the work of ONE whole workgroup of NT threads (its own kernel, or the last
+// part of the lanes fix-up launch, LMODE 2).
+template <int NB, int NT>
+__device__ __forceinline__ void epilogue_block(const EpiArgs& E, const SmfBins& bins) {
+  __shared__ double scratch[NB * (NT / kWave)];
   __shared__ float Sv[kXMaxFloats];
   __shared__ float g[kMaxBins];
   __shared__ float d2[kMaxBins];
+  const float* __restrict__ slab = E.slab;
+  const int nrows = E.nrows, nb = E.nb;
   double v[NB];
 #pragma unroll
   for (int k = 0; k < NB; ++k) v[k] = 0.0;
   // rows four at a time with every load issued before the first add (one memory round trip
   // per four rows instead of one per row); the per-thread order of the sums is unchanged
   int r = threadIdx.x;
-  for (; r + 3 * kEpiThreads < nrows; r += 4 * kEpiThreads) {
+  for (; r + 3 * NT < nrows; r += 4 * NT) {
     float a[4][NB];
 #pragma unroll
     for (int u = 0; u < 4; ++u)
 #pragma unroll
-      for (int k = 0; k < NB; ++k) a[u][k] = slab[(int64_t)(r + u * kEpiThreads) * NB + k];
+      for (int k = 0; k < NB; ++k) a[u][k] = slab[(int64_t)(r + u * NT) * NB + k];
 #pragma unroll
     for (int u = 0; u < 4; ++u)
 #pragma unroll
       for (int k = 0; k < NB; ++k) v[k] += (double)a[u][k];
   }
-  for (; r < nrows; r += kEpiThreads) {
+  for (; r < nrows; r += NT) {
 #pragma unroll
     for (int k = 0; k < NB; ++k) v[k] += (double)slab[(int64_t)r * NB + k];
   }
@@ -410,12 +427,12 @@ __global__ __launch_bounds__(kEpiThreads) void smf_epilogue_kernel(
     for (int k = 0; k < NB; ++k) Sv[k] = (float)(v[k] * (double)bins.scale[k]);
   }
   __syncthreads();
-  if (size > 1) xgmi_block_allreduce(peers, rank, size, Sv, NB, seq, err, ticks);
+  if (E.size > 1) xgmi_block_allreduce(E.peers, E.rank, E.size, Sv, NB, E.seq, E.err, E.ticks);
   const int k = threadIdx.x;
-  if (k < NB) S_out[k] = Sv[k];
+  if (k < NB) E.S_out[k] = Sv[k];
   if (k < nb) {
-    const float s = Sv[k] + eps;
-    const float d = log10f(s) - log10f(target[k] + eps);
+    const float s = Sv[k] + E.eps;
+    const float d = log10f(s) - log10f(E.target[k] + E.eps);
     d2[k] = d * d;
     g[k] = 2.0f / nb * d / (s * kLn10);
   }
@@ -423,12 +440,17 @@ __global__ __launch_bounds__(kEpiThreads) void smf_epilogue_kernel(
   if (k == 0) {
     float acc = 0.0f;
     for (int j = 0; j < nb; ++j) acc += d2[j];
-    loss[0] = acc / nb;
+    E.loss[0] = acc / nb;
   }
-  if (k <= NB) h[k] = k <= nb ? edge_weight(g, bins, k, nb) : 0.0f;
+  if (k <= NB) E.h[k] = k <= nb ? edge_weight(g, bins, k, nb) : 0.0f;
   // the pipelined engine's device step counter, advanced here (the last launch of a step)
   // instead of by a one-thread kernel of its own
-  if (advance != nullptr && threadIdx.x == 0) advance[0] += 1;
+  if (E.advance != nullptr && threadIdx.x == 0) E.advance[0] += 1;
+}
+
+template <int NB>
+__global__ __launch_bounds__(kEpiThreads) void smf_epilogue_kernel(EpiArgs E, SmfBins bins) {
+  epilogue_block<NB, kEpiThreads>(E, bins);
 }
 
 // Per-halo VJP contributions in the scaled coordinate w = z*kWScale:
@@ -1471,7 +1493,7 @@ __global__ __launch_bounds__(kThreads, MG_LANES_MINWAVES) void smf_fwd_lanes_ker
     const int32_t* __restrict__ fwd_order, const float2* __restrict__ theta, int64_t g0,
     int64_t g1, SmfBins bins, float* __restrict__ slab, float* __restrict__ resid,
     const int32_t* __restrict__ wave_start, int* __restrict__ queues, int nq,
-    LanesUpdate upd = LanesUpdate{}, int* __restrict__ defer = nullptr) {
+    LanesUpdate upd = LanesUpdate{}, int* __restrict__ defer = nullptr, EpiArgs epi = EpiArgs{}) {
   static_assert(!UPD || RESID, "the pipelined update reads the residuals it overwrites");
   static_assert(LMODE == 0 || (RESID && MG_FWD_EM && MG_LANES_EP && !REL), "deferral: EM residual forwards");
   static_assert(LMODE != 2 || !UPD, "the fix-up launch evaluates updated groups");
@@ -1870,6 +1892,14 @@ __global__ __launch_bounds__(kThreads, MG_LANES_MINWAVES) void smf_fwd_lanes_ker
       }
     }
   }
+  if constexpr (LMODE == 2) {
+    // single-workgroup fix-up launch with the sumstat epilogue folded in (one launch per
+    // step fewer): this workgroup's own slab row is the last one the epilogue reads
+    if (epi.on) {
+      __syncthreads();
+      epilogue_block<NB, kThreads>(epi, bins);
+    }
+  }
 }
 
 // Residual VJP over slots [s0, s1): whole populations write their gradient, parts of
@@ -2213,45 +2243,63 @@ void smf_logmse(torch::Tensor S, torch::Tensor target, double eps, std::vector<d
 }
 
 // Fused sumstat epilogue (see smf_epilogue_kernel); peers empty = single rank.
-void smf_epilogue(torch::Tensor slab, int64_t nrows, std::vector<double> edges,
-                  std::vector<double> scale, torch::Tensor target, double eps, torch::Tensor S,
-                  torch::Tensor loss, torch::Tensor h, std::vector<int64_t> peers, int64_t rank,
-                  c10::optional<torch::Tensor> seq, c10::optional<torch::Tensor> err,
-                  double timeout_s, c10::optional<torch::Tensor> advance) {
+static EpiArgs make_epi(torch::Tensor slab, int64_t nrows, int nb, int nbp, torch::Tensor target,
+                        double eps, torch::Tensor S, torch::Tensor loss, torch::Tensor h,
+                        const std::vector<int64_t>& peers, int64_t rank, int* seq, int* err,
+                        double timeout_s, int* adv) {
   check_dev(slab, "slab", at::kFloat);
-  int* adv = nullptr;
-  if (advance.has_value()) {
-    TORCH_CHECK(advance->is_cuda() && advance->scalar_type() == at::kInt, "advance: int32 device");
-    adv = advance->data_ptr<int>();
-  }
   check_dev(target, "target", at::kFloat);
   check_dev(S, "S", at::kFloat);
   check_dev(loss, "loss", at::kFloat);
   check_dev(h, "h", at::kFloat);
-  const int nb = (int)scale.size();
-  const int nbp = padded_bins(nb);
   TORCH_CHECK(slab.numel() >= nrows * nbp && nrows >= 1, "slab too small");
   TORCH_CHECK(S.numel() >= nbp && target.numel() >= nb && h.numel() >= nbp + 1, "bad sizes");
   TORCH_CHECK(nbp <= kXMaxFloats, "too many bins for the one-shot exchange");
   const int size = peers.empty() ? 1 : (int)peers.size();
   TORCH_CHECK(size <= kXMaxRanks && rank >= 0 && rank < size, "bad rank/size");
-  XgmiPeers p;
-  for (int r = 0; r < kXMaxRanks; ++r) p.base[r] = r < (int)peers.size() ? reinterpret_cast<char*>(peers[r]) : nullptr;
-  unsigned* sq = nullptr;
-  int* er = nullptr;
-  if (size > 1) {
-    TORCH_CHECK(seq.has_value() && err.has_value(), "multi-rank epilogue needs seq/err");
-    sq = reinterpret_cast<unsigned*>(seq->data_ptr<int>());
-    er = err->data_ptr<int>();
+  EpiArgs E{};
+  for (int r = 0; r < kXMaxRanks; ++r)
+    E.peers.base[r] = r < (int)peers.size() ? reinterpret_cast<char*>(peers[r]) : nullptr;
+  if (size > 1) TORCH_CHECK(seq != nullptr && err != nullptr, "multi-rank epilogue needs seq/err");
+  E.slab = slab.data_ptr<float>();
+  E.nrows = (int)nrows;
+  E.nb = nb;
+  E.rank = (int)rank;
+  E.size = size;
+  E.on = 1;
+  E.seq = reinterpret_cast<unsigned*>(seq);
+  E.err = err;
+  E.ticks = (long long)(timeout_s * 1e8);
+  E.target = target.data_ptr<float>();
+  E.eps = (float)eps;
+  E.S_out = S.data_ptr<float>();
+  E.loss = loss.data_ptr<float>();
+  E.h = h.data_ptr<float>();
+  E.advance = adv;
+  return E;
+}
+
+void smf_epilogue(torch::Tensor slab, int64_t nrows, std::vector<double> edges,
+                  std::vector<double> scale, torch::Tensor target, double eps, torch::Tensor S,
+                  torch::Tensor loss, torch::Tensor h, std::vector<int64_t> peers, int64_t rank,
+                  c10::optional<torch::Tensor> seq, c10::optional<torch::Tensor> err,
+                  double timeout_s, c10::optional<torch::Tensor> advance) {
+  int* adv = nullptr;
+  if (advance.has_value()) {
+    TORCH_CHECK(advance->is_cuda() && advance->scalar_type() == at::kInt, "advance: int32 device");
+    adv = advance->data_ptr<int>();
   }
+  const int nb = (int)scale.size();
+  const int nbp = padded_bins(nb);
+  int* sq = (seq.has_value() && seq->defined()) ? seq->data_ptr<int>() : nullptr;
+  int* er = (err.has_value() && err->defined()) ? err->data_ptr<int>() : nullptr;
+  const EpiArgs E = make_epi(slab, nrows, nb, nbp, target, eps, S, loss, h, peers, rank,
+                             peers.size() > 1 ? sq : nullptr, peers.size() > 1 ? er : nullptr,
+                             timeout_s, adv);
   const SmfBins b = make_bins(edges, scale, nbp);
   auto stream = at::hip::getCurrentHIPStream();
-  const long long ticks = (long long)(timeout_s * 1e8);
   MG_DISPATCH_NB(nbp, {
-    hipLaunchKernelGGL((smf_epilogue_kernel<NB>), dim3(1), dim3(kEpiThreads), 0, stream,
-                       slab.data_ptr<float>(), (int)nrows, nb, b, p, (int)rank, size, sq, er, ticks,
-                       target.data_ptr<float>(), (float)eps, S.data_ptr<float>(),
-                       loss.data_ptr<float>(), h.data_ptr<float>(), adv);
+    hipLaunchKernelGGL((smf_epilogue_kernel<NB>), dim3(1), dim3(kEpiThreads), 0, stream, E, b);
   });
 }
 
@@ -2424,7 +2472,7 @@ void smf_lanes_pack(torch::Tensor xs, torch::Tensor slot_src, torch::Tensor slot
 }
 
 // Forward over groups [g0, g1) of the lanes layout; optional residuals [ngroups, 2(NBP+1), 64].
-void smf_forward_lanes(torch::Tensor xi, torch::Tensor slot_pop, torch::Tensor group_base,
+int64_t smf_forward_lanes(torch::Tensor xi, torch::Tensor slot_pop, torch::Tensor group_base,
                        torch::Tensor group_len, torch::Tensor fwd_order, torch::Tensor theta,
                        std::vector<double> edges,
                        std::vector<double> scale, bool log_sigma, int64_t g0, int64_t g1,
@@ -2435,7 +2483,9 @@ void smf_forward_lanes(torch::Tensor xi, torch::Tensor slot_pop, torch::Tensor g
                        c10::optional<torch::Tensor> queues,
                        c10::optional<std::vector<torch::Tensor>> update,
                        std::vector<double> update_scalars,
-                       c10::optional<torch::Tensor> defer, int64_t fix_blocks) {
+                       c10::optional<torch::Tensor> defer, int64_t fix_blocks,
+                       std::vector<torch::Tensor> epi_tensors, std::vector<double> epi_scalars,
+                       std::vector<int64_t> epi_peers) {
   check_dev(xi, "xi", at::kFloat);
   check_dev(slot_pop, "slot_pop", at::kInt);
   check_dev(group_base, "group_base", at::kLong);
@@ -2500,20 +2550,45 @@ void smf_forward_lanes(torch::Tensor xi, torch::Tensor slot_pop, torch::Tensor g
   }
   const bool lmode = dp != nullptr && MG_FWD_EM && MG_LANES_EP && MG_LANES_DEFER && !rel_tail &&
                      b.delta > 0.0f;
+  // Sumstat epilogue folded into this launch sequence (epi_tensors = [slab of all chunks,
+  // target, S, loss, h, seq, err, advance] (empty = absent), epi_scalars = [rows before this
+  // chunk, eps, rank, timeout_s], epi_peers): the fix-up launch becomes one workgroup that
+  // ends with the epilogue, so a step has no separate epilogue launch; without a fix-up
+  // launch (no deferral) the epilogue kernel runs on its own.
+  const bool with_epi = !epi_tensors.empty();
+  EpiArgs epi{};
+  int64_t fixb = lmode ? (with_epi ? 1 : fix_blocks) : 0;
+  if (with_epi) {
+    TORCH_CHECK(epi_tensors.size() == 8 && epi_scalars.size() == 4, "epilogue: 8 tensors, 4 scalars");
+    auto ptr_i = [](const torch::Tensor& t) -> int* {
+      return t.defined() && t.numel() ? t.data_ptr<int>() : nullptr;
+    };
+    const int64_t row0 = (int64_t)epi_scalars[0];
+    TORCH_CHECK(row0 >= 0, "bad row offset");
+    epi = make_epi(epi_tensors[0], row0 + nblocks + fixb, (int)scale.size(), nbp, epi_tensors[1],
+                   epi_scalars[1], epi_tensors[2], epi_tensors[3], epi_tensors[4], epi_peers,
+                   (int64_t)epi_scalars[2], ptr_i(epi_tensors[5]), ptr_i(epi_tensors[6]),
+                   epi_scalars[3], ptr_i(epi_tensors[7]));
+    TORCH_CHECK(epi.slab + row0 * nbp == slab.data_ptr<float>(),
+                "the chunk's slab must start at the row offset of the full slab");
+  }
   auto fixup = [&]() {
-    if (dp == nullptr) return;
-    float* fs = slab.data_ptr<float>() + nblocks * nbp;
     if (!lmode) {
-      hipMemsetAsync(fs, 0, sizeof(float) * fix_blocks * nbp, stream);
+      if (with_epi)
+        MG_DISPATCH_NB(nbp, {
+          hipLaunchKernelGGL((smf_epilogue_kernel<NB>), dim3(1), dim3(kEpiThreads), 0, stream, epi, b);
+        });
       return;
     }
+    float* fs = slab.data_ptr<float>() + nblocks * nbp;
     MG_DISPATCH_NB(nbp, {
       with_bool(log_sigma, [&](auto LS) {
         hipLaunchKernelGGL((smf_fwd_lanes_kernel<NB, decltype(LS)::value, false, true, false, 2>),
-                           dim3(fix_blocks), dim3(kThreads), 0, stream, xi.data_ptr<float>(),
+                           dim3(fixb), dim3(kThreads), 0, stream, xi.data_ptr<float>(),
                            slot_pop.data_ptr<int32_t>(), group_base.data_ptr<int64_t>(),
                            group_len.data_ptr<int32_t>(), fwd_order.data_ptr<int32_t>(), tp,
-                           (int64_t)0, (int64_t)0, b, fs, rp, nullptr, nullptr, 0, LanesUpdate{}, dp);
+                           (int64_t)0, (int64_t)0, b, fs, rp, nullptr, nullptr, 0, LanesUpdate{}, dp,
+                           epi);
       });
     });
   };
@@ -2570,7 +2645,7 @@ void smf_forward_lanes(torch::Tensor xi, torch::Tensor slot_pop, torch::Tensor g
     fixup();  // after the update: the listed groups are evaluated at their new parameters
     if (u.host_step < 0 && !defer_advance)
       hipLaunchKernelGGL(smf_advance_step_kernel, dim3(1), dim3(1), 0, stream, U[3].data_ptr<int>());
-    return;
+    return nblocks + fixb;
   }
   MG_DISPATCH_NB(nbp, {
     with_bool(log_sigma, [&](auto LS) {
@@ -2592,6 +2667,7 @@ void smf_forward_lanes(torch::Tensor xi, torch::Tensor slot_pop, torch::Tensor g
     });
   });
   fixup();
+  return nblocks + fixb;
 }
 
 // Residual VJP over slots [s0, s1) plus the fixed-order finalize of split populations

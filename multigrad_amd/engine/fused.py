@@ -701,20 +701,37 @@ class FusedAdamEngine:
         fused_ok = (fused is not None and self.fuse_epilogue
                     and (self.size == 1 or self.oneshot is not None) and self.slab.is_cuda)
         advance = None
+        # the epilogue can ride on the last chunk's forward launches (one launch per step
+        # fewer; ops/smf.py, csrc/smf.hip LMODE 2 + epilogue_block)
+        fold = fused_ok and _env_flag("MULTIGRAD_FOLD_EPILOGUE", True) and \
+            getattr(md, "engine_forward_epilogue_ok", lambda: False)()
+        chunks = [self.rank] if self.owner else list(range(self.C))
+        folded = False
         with self._ph("forward"):
-            for c in ([self.rank] if self.owner else range(self.C)):
+            for i, c in enumerate(chunks):
                 self._drain(c)
+                epi = None
+                if fold and i == len(chunks) - 1:
+                    epi = dict(slab=self.slab, row0=row, S=self.S, loss=self.loss, h=self.h,
+                               oneshot=self.oneshot if self.size > 1 else None, advance=None)
                 if update:  # the previous step's VJP + Adam, fused into this forward
                     args = self._update_args(self.step_host - 1)
                     if fused_ok and args["host_step"] is None:
                         # device step counter: advanced by the epilogue launch, not a kernel
                         args["defer_advance"] = True
                         advance = args["step"]
+                    if epi is not None:
+                        epi["advance"] = advance
+                    kw = {} if epi is None else {"epilogue": epi}
                     n = md.engine_forward_update_chunk(self.theta, self.slab[row * self.nS:], c,
-                                                       args)
+                                                       args, **kw)
                 else:
-                    n = md.engine_forward_chunk(self.theta, self.slab[row * self.nS:], c)
+                    kw = {} if epi is None else {"epilogue": epi}
+                    n = md.engine_forward_chunk(self.theta, self.slab[row * self.nS:], c, **kw)
+                folded = epi is not None
                 row += n
+        if folded:
+            return
         if fused_ok:
             with self._ph("sumstat_epilogue"):
                 if fused(self.slab, row, self.S, self.loss, self.h, self.oneshot,

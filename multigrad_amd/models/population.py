@@ -262,12 +262,25 @@ class PopulationSMFModel(OnePointModel):
         return self.shard.fwd_rows(max(h1 - h0, 1), self.bins.nb, True, self.bins.rel_tail,
                                    chunk, resid=True)
 
-    def engine_forward_chunk(self, theta, slab, chunk=None) -> int:
+    def engine_forward_chunk(self, theta, slab, chunk=None, epilogue=None) -> int:
         # the engine always runs the VJP of a chunk after this forward at the same theta,
         # so the forward stores the VJP residuals (lanes layout) -- unless the VJP
         # recomputes (local slot order: few halos per population)
         return smf_forward_slab(theta, self.shard, self.bins, True, slab, chunk,
-                                resid=not self.shard.vjp_recompute, order=self._engine_order())
+                                resid=not self.shard.vjp_recompute, order=self._engine_order(),
+                                epilogue=self._epilogue_spec(epilogue))
+
+    def engine_forward_epilogue_ok(self) -> bool:
+        """The sumstat epilogue can ride on the last forward launch sequence of a step
+        (lanes layout on a GPU): ``engine_forward_*chunk(..., epilogue=...)``."""
+        return self.shard.device.type == "cuda" and self.shard.layout == "lanes" and \
+            not self.shard.vjp_recompute
+
+    def _epilogue_spec(self, e):
+        if e is None:
+            return None
+        return dict(e, target=self.aux_data["target_sumstats"],
+                    eps=float(self.aux_data["loss_eps"]))
 
     def engine_prepare(self, chunks):
         """Host-side schedule construction for the given chunks (called by the engine
@@ -285,12 +298,13 @@ class PopulationSMFModel(OnePointModel):
             (sh.chunk_giant[chunk], sh.chunk_giant[chunk + 1])
         return k1 == k0
 
-    def engine_forward_update_chunk(self, theta, slab, chunk, update: dict) -> int:
+    def engine_forward_update_chunk(self, theta, slab, chunk, update: dict, epilogue=None) -> int:
         """Forward of ``chunk`` that first applies the pending VJP + Adam of the previous
         step per population (``update``: h, m, v, unit_offset, step, host_step, lr, b1, b2,
         eps, traj, traj_stride) -- one pass instead of a VJP kernel plus a forward."""
         return smf_forward_slab(theta, self.shard, self.bins, True, slab, chunk, resid=True,
-                                order=self._engine_order(), update=update)
+                                order=self._engine_order(), update=update,
+                                epilogue=self._epilogue_spec(epilogue))
 
     def engine_reduce(self, slab, nrows, S):
         return smf_slab_reduce(slab, nrows, self.bins, S)

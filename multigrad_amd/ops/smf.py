@@ -446,7 +446,8 @@ def _user_theta(theta: torch.Tensor, shard: PopulationShard, order: str) -> torc
 
 def smf_forward_slab(theta: torch.Tensor, shard: PopulationShard, bins: SmfBins, log_sigma: bool,
                      slab: torch.Tensor, chunk: Optional[int] = None, resid: bool = False,
-                     order: str = "user", update: Optional[dict] = None) -> int:
+                     order: str = "user", update: Optional[dict] = None,
+                     epilogue: Optional[dict] = None) -> int:
     """Forward of the shard (or one population chunk) into per-workgroup slab rows;
     returns the number of rows written.  CPU: one row from the PyTorch reference.
     ``resid`` (lanes layout): also store the VJP residuals of these populations.
@@ -480,16 +481,28 @@ def smf_forward_slab(theta: torch.Tensor, shard: PopulationShard, bins: SmfBins,
             usc = [float(u["unit_offset"]), float(-1 if u.get("host_step") is None else u["host_step"]),
                    float(u["lr"]), float(u["b1"]), float(u["b2"]), float(u["eps"]),
                    float(u.get("traj_stride", 0)), float(bool(u.get("defer_advance", False)))]
-        ext().smf_forward_lanes(shard.xi, shard.slot_index(order), shard.group_base,
-                                shard.group_len, shard.fwd_order, theta, list(bins.edges),
-                                list(bins.scale), bool(log_sigma), g0, g1, slab, nblk,
-                                bins.rel_tail, rbuf, w_order, w_start, queues, upd, usc,
-                                shard.defer_buffer() if resid else None,
-                                LANES_FIX_BLOCKS if resid else 0)
+        et, es, ep = [], [], []
+        if epilogue is not None:  # the sumstat epilogue folded into this launch sequence
+            e = epilogue
+            none = torch.empty(0, dtype=torch.int32, device=theta.device)
+            os_ = e.get("oneshot")
+            adv = e.get("advance")
+            et = [e["slab"], e["target"], e["S"], e["loss"], e["h"],
+                  none if os_ is None else os_.seq, none if os_ is None else os_.err,
+                  none if adv is None else adv]
+            es = [float(e["row0"]), float(e["eps"]), float(0 if os_ is None else os_.rank),
+                  float(5.0 if os_ is None else os_.timeout_s)]
+            ep = [] if os_ is None else list(os_.peers)
+        rows = ext().smf_forward_lanes(shard.xi, shard.slot_index(order), shard.group_base,
+                                       shard.group_len, shard.fwd_order, theta, list(bins.edges),
+                                       list(bins.scale), bool(log_sigma), g0, g1, slab, nblk,
+                                       bins.rel_tail, rbuf, w_order, w_start, queues, upd, usc,
+                                       shard.defer_buffer() if resid else None,
+                                       LANES_FIX_BLOCKS if resid else 0, et, es, ep)
         if resid:
             shard.resid_epoch += 1
-            return nblk + LANES_FIX_BLOCKS
-        return nblk
+        return int(rows)
+    assert epilogue is None, "the folded epilogue is a lanes-layout launch"
     ext().smf_forward(shard.x, shard.pop, theta, list(bins.edges), list(bins.scale),
                       bool(log_sigma), h0, h1, slab, nblk, bins.rel_tail)
     return nblk
