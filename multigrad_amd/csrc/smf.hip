@@ -1895,7 +1895,7 @@ __global__ __launch_bounds__(kThreads, MG_LANES_MINWAVES) void smf_fwd_lanes_ker
   if constexpr (LMODE == 2) {
     // single-workgroup fix-up launch with the sumstat epilogue folded in (one launch per
     // step fewer): this workgroup's own slab row is the last one the epilogue reads
-    if (epi.on) {
+    if (epi.on && gridDim.x == 1) {  // (the host launches the folded form with one workgroup)
       __syncthreads();
       epilogue_block<NB, kThreads>(epi, bins);
     }
