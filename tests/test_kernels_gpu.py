@@ -350,6 +350,33 @@ def test_fused_epilogue_matches_separate_kernels(graph):
     torch.testing.assert_close(eng.h, sep.h, rtol=1e-6, atol=1e-12)
 
 
+@pytest.mark.parametrize("narrow", [False, True])
+def test_folded_epilogue_matches_separate_launch(monkeypatch, narrow):
+    """The sumstat epilogue folded into the single-workgroup fix-up launch of the deferred
+    lanes groups (MULTIGRAD_FOLD_EPILOGUE) against the separate epilogue launch, pipelined,
+    with no group deferred and with narrow populations that the fix-up must evaluate; the
+    deferral list is left at zero after every step."""
+    from multigrad_amd.engine.fused import FusedAdamEngine
+    from multigrad_amd.models.population import PopulationSMFModel, make_population_data
+    data = make_population_data(num_params=6000, num_halos=300_000, seed=21, device=DEV)
+    model = PopulationSMFModel(aux_data=data)
+    model.set_target_from_truth()
+    guess = _narrow_guess(data, every=3) if narrow else data["guess"]
+    out = {}
+    for fold in ("0", "1"):
+        monkeypatch.setenv("MULTIGRAD_FOLD_EPILOGUE", fold)
+        eng = FusedAdamEngine(model, graph=False)
+        out[fold] = (eng.run_adam(guess, nsteps=5, learning_rate=1e-3), eng.loss.clone(), eng.h.clone())
+        assert eng.pipeline
+        assert int(data["shard"].defer_buffer()[:2].abs().sum()) == 0
+    torch.testing.assert_close(out["1"][0], out["0"][0], rtol=1e-6, atol=1e-7)
+    torch.testing.assert_close(out["1"][1], out["0"][1], rtol=1e-6, atol=0)
+    # h: differences of cotangent terms, so an ulp of S (the slab rows are grouped
+    # differently per thread: one fix-up row instead of eight) shows up at ~1e-6 relative
+    torch.testing.assert_close(out["1"][2], out["0"][2], rtol=1e-5,
+                               atol=1e-6 * float(out["0"][2].abs().max()))
+
+
 @pytest.mark.parametrize("owner,graph,history", [(False, True, "full"), (False, False, "full"),
                                                  (False, True, "last"), (True, False, "full"),
                                                  (True, True, 2)])
