@@ -915,9 +915,13 @@ __device__ __forceinline__ EmLane em_lane(float inv, float delta) {
 }
 
 // One halo (nm = -(x + a) inv): F, Wa, E accumulate the UNSCALED sums of edge pairs (the
-// pair layout of EdgePairs; an odd last edge in the .x half of the extra pair).
+// pair layout of EdgePairs; an odd last edge in the .x half of the extra pair).  The lane
+// constants come as scalars, not as the EmLane struct: splats of adjacent struct fields were
+// widened into 8-byte loads that kept (a1, a3, a5) in private memory, a scratch store and two
+// scratch loads at every group start of the headline kernel.
 template <int NB, bool RESID>
-__device__ __forceinline__ void em_halo(float nm, const EmLane& L, const SmfBins& b,
+__device__ __forceinline__ void em_halo(float nm, float inv, float dw4, float a1, float a3,
+                                        float a5, const SmfBins& b,
                                         v2f (&F)[EdgePairs<NB>::NV], v2f (&Wa)[EdgePairs<NB>::NV],
                                         v2f (&E)[EdgePairs<NB>::NV]) {
   using EP = EdgePairs<NB>;
@@ -926,13 +930,13 @@ __device__ __forceinline__ void em_halo(float nm, const EmLane& L, const SmfBins
   nm = __builtin_amdgcn_fmed3f(nm, -1e6f, 1e6f);
   // w of the seed pair from the edges; the other pairs step by 2 dw (two lane constants
   // instead of one per pair, which the compiler would otherwise keep in registers)
-  const float dw2 = -0.5f * L.dw4;
+  const float dw2 = -0.5f * dw4;
   v2f wm;
   {
     v2f e2;
     e2.x = b.edge[2 * M];
     e2.y = b.edge[2 * M + 1];
-    wm = e2 * L.inv + nm;
+    wm = e2 * inv + nm;
   }
   auto wpair = [&](int i) { return wm + (float)(i - M) * dw2; };
   auto accum = [&](int i, v2f p, v2f w) {
@@ -940,8 +944,8 @@ __device__ __forceinline__ void em_halo(float nm, const EmLane& L, const SmfBins
     F[i] = F[i] + p;
     if constexpr (RESID) Wa[i] = Wa[i] + pw;
     const v2f w2 = w * w;
-    v2f t = w2 * L.a5 + L.a3;
-    t = t * w2 + L.a1;
+    v2f t = w2 * a5 + a3;
+    t = t * w2 + a1;
     E[i] = pw * t + E[i];
   };
   const v2f ws = wpair(M);
@@ -949,7 +953,7 @@ __device__ __forceinline__ void em_halo(float nm, const EmLane& L, const SmfBins
   v2f p0;
   p0.x = fast_exp2(q.x);
   p0.y = fast_exp2(q.y);
-  const float R = fast_exp2(__builtin_amdgcn_fmed3f(L.dw4 * ws.y, -126.0f, 126.0f));
+  const float R = fast_exp2(__builtin_amdgcn_fmed3f(dw4 * ws.y, -126.0f, 126.0f));
   accum(M, p0, ws);
   v2f p = p0;
 #pragma unroll
@@ -964,7 +968,7 @@ __device__ __forceinline__ void em_halo(float nm, const EmLane& L, const SmfBins
     F[EP::NP].x += pz;
     if constexpr (RESID) Wa[EP::NP].x += pw;
     const float w2 = wz * wz;
-    const float t = fmaf(fmaf(w2, L.a5, L.a3), w2, L.a1);
+    const float t = fmaf(fmaf(w2, a5, a3), w2, a1);
     E[EP::NP].x = fmaf(pw, t, E[EP::NP].x);
   }
   if constexpr (M > 0) {
@@ -988,7 +992,7 @@ __device__ __forceinline__ void lane_halo_em(float x, const EmLane& L, float nma
                                              const SmfBins& b, v2f (&F)[EdgePairs<NB>::NV],
                                              v2f (&Wa)[EdgePairs<NB>::NV],
                                              v2f (&E)[EdgePairs<NB>::NV]) {
-  em_halo<NB, RESID>(fmaf(x, -L.inv, nma), L, b, F, Wa, E);
+  em_halo<NB, RESID>(fmaf(x, -L.inv, nma), L.inv, L.dw4, L.a1, L.a3, L.a5, b, F, Wa, E);
 #if MG_EM_SCHED_BARRIER
   __builtin_amdgcn_sched_barrier(0);
 #endif
