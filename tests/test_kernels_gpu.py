@@ -53,6 +53,31 @@ def test_population_forward_and_vjp_match_fp64(nbins, giant, layout):
                                atol=2e-5 * float(gref.abs().max()))
 
 
+@pytest.mark.parametrize("logsig", [-0.4, -0.45, -0.55])
+def test_em_forward_bin_width_ranges_vs_fp64(logsig):
+    """Edges 0.1 apart and log10 sigma = logsig +- 0.1: bin widths in sigma units of
+    0.20-0.32 (the headline guess), 0.22-0.35 and 0.28-0.45 on the Euler-Maclaurin path --
+    forward and VJP against the fp64 oracle."""
+    n, npop = 400_000, 2000
+    x, pop = _rand_shard(n, npop, seed=7)  # x + a in [7.9, 9.1]: the bins 8.5..9.5 sit on it
+    theta64 = _theta(npop, seed=8)
+    theta64[1::2] += logsig + 0.5
+    bins = S.SmfBins.make(np.linspace(8.5, 9.5, 11), volume=1e4)
+    shard = S.PopulationShard(x.float(), pop.int().to(DEV), npop, device=DEV, chunks=2,
+                              layout="lanes")
+    xf = x.float().double()
+    th_ref = theta64.float().double().requires_grad_(True)
+    ref = S.smf_sumstats_reference(th_ref, xf, pop, bins, log_sigma=True)
+    gS = torch.linspace(0.5, 1.5, 10, dtype=torch.float64)
+    (gref,) = torch.autograd.grad(ref, th_ref, gS)
+    th = theta64.float().to(DEV).requires_grad_(True)
+    out = S.smf_sumstats(th, shard, bins, log_sigma=True)
+    (gk,) = torch.autograd.grad(out, th, gS.float().to(DEV))
+    np.testing.assert_allclose(out.detach().cpu().double(), ref.detach(), rtol=2e-5, atol=1e-12)
+    np.testing.assert_allclose(gk.cpu().double(), gref, rtol=2e-4,
+                               atol=2e-5 * float(gref.abs().max()))
+
+
 @pytest.mark.parametrize("tail", ["relative", "absolute"])
 @pytest.mark.parametrize("log_sigma", [False, True])
 def test_shared_params_model_kernel(log_sigma, tail):
@@ -370,7 +395,9 @@ def test_folded_epilogue_matches_separate_launch(monkeypatch, narrow):
         assert eng.pipeline
         assert int(data["shard"].defer_buffer()[:2].abs().sum()) == 0
     torch.testing.assert_close(out["1"][0], out["0"][0], rtol=1e-6, atol=1e-7)
-    torch.testing.assert_close(out["1"][1], out["0"][1], rtol=1e-6, atol=0)
+    # the two schedules reduce different numbers of slab rows (1 fix-up row vs
+    # MULTIGRAD_FIX_BLOCKS), so the float sums differ in order
+    torch.testing.assert_close(out["1"][1], out["0"][1], rtol=1e-5, atol=0)
     # h: differences of cotangent terms, so an ulp of S (the slab rows are grouped
     # differently per thread: one fix-up row instead of eight) shows up at ~1e-6 relative
     torch.testing.assert_close(out["1"][2], out["0"][2], rtol=1e-5,
