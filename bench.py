@@ -63,6 +63,10 @@ def _args(argv=None):
     ap.add_argument("--lane-order", default="auto", choices=["auto", "global", "local"],
                     help="lanes layout slot order (auto: local for hashed shards on several "
                          "ranks, global otherwise)")
+    ap.add_argument("--narrow-frac", type=float, default=0.0,
+                    help="fraction of populations (scattered by a hash) with a narrow true "
+                         "sigma (bin width > 0.5 sigma: outside the Euler-Maclaurin forward's "
+                         "range, evaluated by the per-edge path); the headline is 0")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--profile-phases", action="store_true")
     ap.add_argument("--no-count-launches", dest="count_launches", action="store_false",
@@ -130,7 +134,8 @@ def time_placement(placement, args, comm, dev, sync):
     data = make_population_data(args.params, args.halos, seed=1234, comm=comm, device=dev,
                                 placement=placement if comm.size > 1 else "hashed",
                                 layout=args.layout,
-                                lane_order=None if args.lane_order == "auto" else args.lane_order)
+                                lane_order=None if args.lane_order == "auto" else args.lane_order,
+                                narrow_frac=args.narrow_frac)
     model = PopulationSMFModel(aux_data=data, comm=comm)
     model.set_target_from_truth()
     history = args.history if args.history in ("full", "last") else int(args.history)
@@ -143,6 +148,7 @@ def time_placement(placement, args, comm, dev, sync):
                  learning_rate=args.lr, history=history)
     sync()
     setup_s = time.perf_counter() - t_setup
+    fb = model.lane_fallback_groups(data["guess"])
 
     for _ in range(args.warmup):
         engine.step()
@@ -190,6 +196,7 @@ def time_placement(placement, args, comm, dev, sync):
         "loss_first_timed": loss0,
         "loss_last": loss1,
         "setup_s": round(setup_s, 2),
+        "fallback_groups": list(fb),
         "history": history,
         "device_ops_per_step": ops or None,
         "autotune": getattr(engine, "tuning", None),
@@ -296,6 +303,8 @@ def main(argv=None):
             "sumstat_allreduce": head["sumstat_allreduce"],
             "chunks": head["chunks"],
             "layout": head["layout"],
+            "narrow_frac": args.narrow_frac,
+            "per_edge_groups": head["fallback_groups"],
             "device_ops_per_step": head["device_ops_per_step"],
             "autotune": head["autotune"],
         },

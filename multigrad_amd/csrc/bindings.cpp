@@ -23,6 +23,7 @@ void smf_vjp(torch::Tensor x, c10::optional<torch::Tensor> pop, torch::Tensor th
              std::vector<double> edges, std::vector<double> scale, bool log_sigma,
              torch::Tensor grad, torch::Tensor partials, torch::Tensor giant);
 int64_t smf_fwd_lanes_max_blocks(int64_t nb, bool log_sigma, bool rel_tail, bool resid);
+int64_t smf_lanes_fallback_mode();
 void smf_lanes_pack(torch::Tensor xs, torch::Tensor slot_src, torch::Tensor slot_len,
                     torch::Tensor group_base, torch::Tensor group_len, torch::Tensor xi);
 int64_t smf_forward_lanes(torch::Tensor xi, torch::Tensor slot_pop, torch::Tensor group_base,
@@ -127,6 +128,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("smf_vjp", &mg::smf_vjp);
   m.def("smf_fwd_lanes_max_blocks", &mg::smf_fwd_lanes_max_blocks);
   m.def("smf_lanes_pack", &mg::smf_lanes_pack);
+  m.def("smf_lanes_fallback_mode", &mg::smf_lanes_fallback_mode);
   m.def("smf_forward_lanes", &mg::smf_forward_lanes, pybind11::arg("xi"), pybind11::arg("slot_pop"),
         pybind11::arg("group_base"), pybind11::arg("group_len"), pybind11::arg("fwd_order"),
         pybind11::arg("theta"), pybind11::arg("edges"), pybind11::arg("scale"),

@@ -1353,9 +1353,17 @@ __global__ __launch_bounds__(kThreads, MG_VJP_REC_MINWAVES) void smf_vjp_tiles_r
 #ifndef MG_LANES_EP
 #define MG_LANES_EP 1
 #endif
+// How the Euler-Maclaurin residual forwards evaluate a group outside the EM range:
+//   0: inline per-edge fallback (LMODE 0; costs the hot loop registers and spills),
+//   1: deferral list + fix-up launch (LMODE 1 + 2, round 3; the fix-up launch is narrow),
+//   2: out-of-line per-edge call inside the main launch (LMODE 3, default): full machine
+//      parallelism at any deferral fraction, no fix-up launch, no list atomics.
 #ifndef MG_LANES_DEFER
-#define MG_LANES_DEFER 1  // residual forwards defer groups outside the EM range (LMODE 1)
+#define MG_LANES_DEFER 2
 #endif
+// LMODE of the main launch of the EM residual forwards (0 in builds without them)
+constexpr int kLanesMainMode =
+    !(MG_FWD_EM && MG_LANES_EP) ? 0 : MG_LANES_DEFER == 1 ? 1 : MG_LANES_DEFER == 2 ? 3 : 0;
 
 // Packed two-halo path: 10% fewer VALU cycles per halo pair, but it needs 108 VGPRs
 // (4 waves/SIMD) to avoid spills; measured on MI355X it ties the scalar path (690 vs
@@ -1483,7 +1491,76 @@ __device__ __forceinline__ void lds_stage_block(const float* src, float* dst, in
                     std::make_integer_sequence<int, NR % 4>{});
 }
 
-// LMODE (Euler-Maclaurin residual forwards, MG_LANES_DEFER): 0 = plain; 1 = DEFER: a group
+// LMODE 3: ONE whole lanes group by per-edge tails (the groups outside the Euler-Maclaurin
+// range), out of line.  The main kernel's registers are sized by its hot EM loop; a call
+// keeps this path's live ranges out of that allocation (the callee saves what it clobbers,
+// on the cold path only), where the inline fallback cost spills (126 VGPRs, 8 spilled) and
+// the deferral list of round 3 ran the out-of-range groups on a narrow fix-up launch.
+// Per-edge accumulators in the edge-pair layout of lane_halo_ep (signed tails, wave counts
+// by ballot); the residuals G, W are stored here, in the group-major layout of the kernel.
+template <int NB>
+struct LaneGroupSums {
+  v2f acc[EdgePairs<NB>::NV];
+  int cnt[NB + 1];
+};
+
+template <int NB>
+__device__ __attribute__((noinline)) LaneGroupSums<NB> lanes_group_exact(
+    const float* __restrict__ xg, int len, float x0, float x1, float ninv, float mua, float e0,
+    float delta, float* __restrict__ rg) {
+  using EP = EdgePairs<NB>;
+  const int lane = threadIdx.x & (kWave - 1);
+  // uniform edges from (e0, delta) in registers: a reference to the kernel's SmfBins would
+  // make the kernel copy the whole struct to private memory at its start
+  SmfBins b;
+#pragma unroll
+  for (int e = 0; e <= NB; ++e) b.edge[e] = fmaf((float)e, delta, e0);
+  LaneGroupSums<NB> o;
+  v2f G[EP::NV], W[EP::NV];
+#pragma unroll
+  for (int i = 0; i < EP::NV; ++i) {
+    o.acc[i] = (v2f)(0.0f);
+    G[i] = (v2f)(0.0f);
+    W[i] = (v2f)(0.0f);
+  }
+#pragma unroll
+  for (int e = 0; e <= NB; ++e) o.cnt[e] = 0;
+  // two halos per iteration with the next pair's loads in flight: buffer loads at a wave-
+  // uniform row offset, unconditional (the rows past a group's end belong to the next group
+  // or to the 16 padding rows of xi) and masked to the sentinel at the use; the first pair
+  // (x0, x1) comes from the caller, which loaded it with the group
+  const __amdgpu_buffer_rsrc_t xr = buf_rsrc(xg);
+  const int voff = lane * 4;
+  for (int j = 0; j < len; j += 2) {
+    const float c0 = x0;
+    const float c1 = j + 1 < len ? x1 : kLaneSentinel;
+    x0 = buf_load_f32(xr, voff, (j + 2) * kWave * 4);
+    x1 = buf_load_f32(xr, voff, (j + 3) * kWave * 4);
+    lane_halo_ep<NB, true, false, true>(c0, c1, ninv, mua, b, o.acc, o.cnt, G, W);
+  }
+  float Gs[NB + 1], Ws[NB + 1];
+#pragma unroll
+  for (int i = 0; i < EP::NP; ++i) {
+    Gs[2 * i] = G[i].x;
+    Gs[2 * i + 1] = G[i].y;
+    Ws[2 * i] = W[i].x;
+    Ws[2 * i + 1] = W[i].y;
+  }
+  if constexpr (EP::NX) {
+    Gs[NB] = G[EP::NP].x + G[EP::NP].y;
+    Ws[NB] = W[EP::NP].x + W[EP::NP].y;
+  }
+  const __amdgpu_buffer_rsrc_t rr = buf_rsrc(rg);
+#pragma unroll
+  for (int e = 0; e <= NB; ++e) {
+    buf_store_f32(rr, voff, e * kWave * 4, Gs[e]);
+    buf_store_f32(rr, voff, (NB + 1 + e) * kWave * 4, Ws[e]);
+  }
+  return o;
+}
+
+// LMODE (Euler-Maclaurin residual forwards, MG_LANES_DEFER): 0 = plain; 3 = CALL: a group
+// outside the EM range is evaluated by lanes_group_exact (out of line); 1 = DEFER: a group
 // outside the EM range is not evaluated here but appended to the device list `defer`
 // ([count, done ticket, group ids...]) -- the kernel then carries no per-edge fallback code
 // (which cost ~3.5% of the headline step in registers although the headline data never
@@ -1769,6 +1846,17 @@ __global__ __launch_bounds__(kThreads, MG_LANES_MINWAVES) void smf_fwd_lanes_ker
         const int slot = atomicAdd(defer, 1);
         defer[2 + slot] = (int)gc;
       }
+    } else if constexpr (LMODE == 3) {
+      if (!em) {  // outside the EM range: per-edge tails, out of line (stores the residuals)
+        const LaneGroupSums<NB> o = lanes_group_exact<NB>(
+            xi + group_base[gc], len, lane_use(xn[0], 0, len), lane_use(xn[1], 1, len), ninv,
+            mua, bins.edge[0], bins.delta,
+            resid + gc * (2 * (NB + 1) * kWave));
+#pragma unroll
+        for (int i = 0; i < EP::NV; ++i) accp[i] = accp[i] + o.acc[i];
+#pragma unroll
+        for (int e = 0; e <= NB; ++e) cnt[e] += __builtin_amdgcn_readfirstlane(o.cnt[e]);
+      }
     } else
 #ifdef MG_FWD_EM_ONLY
     if (!kEm)
@@ -1815,7 +1903,9 @@ __global__ __launch_bounds__(kThreads, MG_LANES_MINWAVES) void smf_fwd_lanes_ker
 #endif
     if constexpr (!UPD)
       if (kn < g1) load_group(kn, c_next);
-    if (RESID && (LMODE != 1 || em)) {  // group-major [g][2 (NB+1)][64]: one block per group
+    // group-major [g][2 (NB+1)][64]: one block per group (LMODE 1: deferred groups are
+    // stored by the fix-up launch; LMODE 3: by lanes_group_exact)
+    if (RESID && ((LMODE != 1 && LMODE != 3) || em)) {
 #if MG_LANES_BUF
       const __amdgpu_buffer_rsrc_t rr = buf_rsrc(resid + gc * (2 * (NB + 1) * kWave));
 #else
@@ -2439,6 +2529,11 @@ torch::Tensor smf_fwd_trace() {
 }
 
 // ------------------------------------------------------------------ lanes host side
+// How the EM residual forwards handle out-of-range groups (MG_LANES_DEFER): 1 = deferral
+// list + fix-up launch (the caller provides the list and fix-up slab rows), 2 = out-of-line
+// call inside the main launch, 0 = inline fallback.
+int64_t smf_lanes_fallback_mode() { return MG_LANES_DEFER; }
+
 int64_t smf_fwd_lanes_max_blocks(int64_t nb, bool log_sigma, bool rel_tail, bool resid) {
   const int nbp = padded_bins((int)nb);
   int dev = 0;
@@ -2538,13 +2633,14 @@ int64_t smf_forward_lanes(torch::Tensor xi, torch::Tensor slot_pop, torch::Tenso
   const SmfBins b = make_bins(edges, scale, nbp);
   auto stream = at::hip::getCurrentHIPStream();
   const float2* tp = reinterpret_cast<const float2*>(theta.data_ptr<float>());
-  // Residual forwards with a deferral list (see LMODE): the main launch defers groups outside
-  // the Euler-Maclaurin range, then a fix-up launch of fix_blocks workgroups evaluates them
-  // into slab rows [nblocks, nblocks + fix_blocks) (zero rows when nothing was deferred).
-  // Without uniform bins every group would be deferred: the main launch keeps its own
-  // per-edge path and the fix-up rows are zeroed.
+  // Residual forwards with a deferral list (MG_LANES_DEFER 1, see LMODE): the main launch
+  // defers groups outside the Euler-Maclaurin range, then a fix-up launch of fix_blocks
+  // workgroups evaluates them into slab rows [nblocks, nblocks + fix_blocks).  Without
+  // uniform bins the main launch keeps its own per-edge path and no fix-up launch runs
+  // (fixb = 0: the rows are neither written nor counted).  With MG_LANES_DEFER 2 the list
+  // is ignored (lanes_fallback_mode() tells the caller not to allocate the rows).
   int* dp = nullptr;
-  if (defer.has_value() && defer->defined()) {
+  if (MG_LANES_DEFER == 1 && defer.has_value() && defer->defined()) {
     TORCH_CHECK(has_resid, "the deferral list is for residual forwards");
     check_dev(*defer, "defer", at::kInt);
     TORCH_CHECK(defer->numel() >= 2 + ng, "defer: [count, ticket, one slot per group]");
@@ -2552,8 +2648,11 @@ int64_t smf_forward_lanes(torch::Tensor xi, torch::Tensor slot_pop, torch::Tenso
     TORCH_CHECK(slab.numel() >= (nblocks + fix_blocks) * nbp, "slab too small for the fix-up rows");
     dp = defer->data_ptr<int>();
   }
-  const bool lmode = dp != nullptr && MG_FWD_EM && MG_LANES_EP && MG_LANES_DEFER && !rel_tail &&
-                     b.delta > 0.0f;
+  // the Euler-Maclaurin residual forwards: out-of-range groups through the out-of-line call
+  // (LMODE 3, MG_LANES_DEFER 2) or the deferral list (LMODE 1 + 2, MG_LANES_DEFER 1)
+  const bool em_resid = has_resid && MG_FWD_EM && MG_LANES_EP && !rel_tail && b.delta > 0.0f;
+  const bool lmode = dp != nullptr && MG_LANES_DEFER == 1 && em_resid;
+  const bool lcall = MG_LANES_DEFER == 2 && em_resid;
   // Sumstat epilogue folded into this launch sequence (epi_tensors = [slab of all chunks,
   // target, S, loss, h, seq, err, advance] (empty = absent), epi_scalars = [rows before this
   // chunk, eps, rank, timeout_s], epi_peers): the fix-up launch becomes one workgroup that
@@ -2584,6 +2683,7 @@ int64_t smf_forward_lanes(torch::Tensor xi, torch::Tensor slot_pop, torch::Tenso
         });
       return;
     }
+    if constexpr (kLanesMainMode == 1) {
     float* fs = slab.data_ptr<float>() + nblocks * nbp;
     MG_DISPATCH_NB(nbp, {
       with_bool(log_sigma, [&](auto LS) {
@@ -2595,6 +2695,7 @@ int64_t smf_forward_lanes(torch::Tensor xi, torch::Tensor slot_pop, torch::Tenso
                            epi);
       });
     });
+    }
   };
   if (update.has_value()) {
     // pipelined update: tensors [h, m, v, step(int32[2]), traj (or empty)]; scalars
@@ -2629,8 +2730,8 @@ int64_t smf_forward_lanes(torch::Tensor xi, torch::Tensor slot_pop, torch::Tenso
     u.step = U[3].data_ptr<int>();
     MG_DISPATCH_NB(nbp, {
       with_bool(log_sigma, [&](auto LS) {
-        if (lmode) {
-          hipLaunchKernelGGL((smf_fwd_lanes_kernel<NB, decltype(LS)::value, false, true, true, MG_LANES_DEFER>),
+        if (lmode || lcall) {
+          hipLaunchKernelGGL((smf_fwd_lanes_kernel<NB, decltype(LS)::value, false, true, true, kLanesMainMode>),
                              dim3(nblocks), dim3(kThreads), 0, stream, xi.data_ptr<float>(),
                              slot_pop.data_ptr<int32_t>(), group_base.data_ptr<int64_t>(),
                              group_len.data_ptr<int32_t>(), order, tp, g0, g1, b,
@@ -2653,8 +2754,8 @@ int64_t smf_forward_lanes(torch::Tensor xi, torch::Tensor slot_pop, torch::Tenso
   }
   MG_DISPATCH_NB(nbp, {
     with_bool(log_sigma, [&](auto LS) {
-      if (lmode) {
-        hipLaunchKernelGGL((smf_fwd_lanes_kernel<NB, decltype(LS)::value, false, true, false, MG_LANES_DEFER>),
+      if (lmode || lcall) {
+        hipLaunchKernelGGL((smf_fwd_lanes_kernel<NB, decltype(LS)::value, false, true, false, kLanesMainMode>),
                            dim3(nblocks), dim3(kThreads), 0, stream, xi.data_ptr<float>(),
                            slot_pop.data_ptr<int32_t>(), group_base.data_ptr<int64_t>(),
                            group_len.data_ptr<int32_t>(), order, tp, g0, g1, b,

@@ -70,8 +70,11 @@ __device__ __forceinline__ void xgmi_block_allreduce(const XgmiPeers& peers, int
   __syncthreads();
   if (t < size) {
     const long long t0 = wall_clock64();
+    // after a timeout the protocol is out of step until reset(): fail fast (NaN) instead of
+    // waiting out the timeout again in every later call
+    const bool dead = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
     while (uc_poll(xflags(me) + slot * kXMaxRanks + t) != seq) {
-      if (wall_clock64() - t0 > timeout_ticks) {
+      if (dead || wall_clock64() - t0 > timeout_ticks) {
         atomicExch(err, 1);
         timed_out = 1;
         break;
@@ -117,8 +120,9 @@ __device__ __forceinline__ unsigned* ts_ticket(char* b) {
 }
 
 // Threads t < size of the calling block wait until flag[t] >= seq (monotonic sequence
-// numbers, wrap-safe difference); returns 1 (and raises *err) on a timeout.  Every thread
-// of the block must call it.
+// numbers, wrap-safe difference); returns 1 (and raises *err) on a timeout -- at once when
+// *err is already raised (a protocol out of step until reset(): no second timeout).  Every
+// thread of the block must call it.
 __device__ __forceinline__ int ts_wait_all(unsigned* flags, int size, unsigned seq, int* err,
                                            long long timeout_ticks) {
   __shared__ int to;
@@ -126,8 +130,9 @@ __device__ __forceinline__ int ts_wait_all(unsigned* flags, int size, unsigned s
   __syncthreads();
   if ((int)threadIdx.x < size) {
     const long long t0 = wall_clock64();
+    const bool dead = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
     while ((int)(uc_poll(flags + threadIdx.x) - seq) < 0) {
-      if (wall_clock64() - t0 > timeout_ticks) {
+      if (dead || wall_clock64() - t0 > timeout_ticks) {
         atomicExch(err, 1);
         to = 1;
         break;

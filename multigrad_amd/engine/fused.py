@@ -45,8 +45,10 @@ Engine protocol (implemented by :class:`~multigrad_amd.models.population.Populat
 ``engine_nS()``, ``engine_fwd_rows(chunk)``, ``engine_forward_chunk(theta, slab, chunk)
 -> rows``, ``engine_reduce(slab, rows, S)``, ``engine_loss_into(S, loss, h)``,
 ``engine_vjp_into(theta, h, grad, chunk)``, optionally ``engine_param_perm()`` (the
-unit order the model wants the engine vectors in).  Every method works on CPU tensors too
-(PyTorch reference math), which is how the multi-rank orchestration is tested on gloo.
+unit order the model wants the engine vectors in) and ``engine_layout_hint(guess)`` (the
+starting parameters, before ``engine_set_chunks``, for a data layout that depends on
+them).  Every method works on CPU tensors too (PyTorch reference math), which is how the
+multi-rank orchestration is tested on gloo.
 """
 from __future__ import annotations
 
@@ -82,6 +84,12 @@ def _side_stream_mode() -> str:
     if v in ("0", "off", "false", "no"):
         return "off"
     return "auto"
+
+
+def _best_ms(tuning) -> float:
+    """Fastest measured candidate of an autotune record (dropped candidates have no time)."""
+    ms = [c["ms"] for c in tuning["candidates"] if c.get("ms") is not None]
+    return min(ms) if ms else math.inf
 
 
 def plan_chunks(J: int, upp: int, world: int, nchunks: int):
@@ -183,7 +191,7 @@ class FusedAdamEngine:
         if not (tun and self.twoshot is not None and not self.owner and self.C == 2
                 and not self._chunks_explicit and "ts_side" in tun["chosen"]):
             return self
-        t2 = min(c["ms"] for c in tun["candidates"])
+        t2 = _best_ms(tun)
         skip = getattr(self, "_skip_autotune", False)
         self._chunks_override = 1
         self._skip_autotune = True
@@ -196,7 +204,7 @@ class FusedAdamEngine:
             cands.append({"ts_side": False, "rccl_exchange": True})
         self._autotune(cands, min_window_s=1e-3 * float(
             os.environ.get("MULTIGRAD_AUTOTUNE_WINDOW_MS", "30")))
-        t1 = min(c["ms"] for c in self.tuning["candidates"])
+        t1 = _best_ms(self.tuning)
         tun1 = self.tuning
         chunk_times = {"1": t1, "2": t2}
         tuned = {1: tun1, 2: tun}
@@ -216,7 +224,7 @@ class FusedAdamEngine:
                 self._autotune([{"ts_side": True, "rccl_exchange": False}],
                                min_window_s=1e-3 * float(
                                    os.environ.get("MULTIGRAD_AUTOTUNE_WINDOW_MS", "30")))
-                chunk_times["4"] = min(c["ms"] for c in self.tuning["candidates"])
+                chunk_times["4"] = _best_ms(self.tuning)
                 tuned[4] = self.tuning
                 current = 4
         best = min(tuned, key=lambda c: chunk_times[str(c)])
@@ -231,6 +239,9 @@ class FusedAdamEngine:
                 setattr(self, k, v)
             self.graph = None
         self.tuning = dict(tuned[best], chunks=dict(chunk_times, chosen=best))
+        dropped = [dict(d, chunks=n) for n, t in tuned.items() for d in t.get("dropped", [])]
+        if dropped:  # candidates dropped in any of the chunk-count tunings, with the reason
+            self.tuning["dropped"] = dropped
         return self
 
     def _setup(self, guess, nsteps: int, param_bounds=None, learning_rate: float = 0.01,
@@ -264,6 +275,9 @@ class FusedAdamEngine:
                 self.twoshot = self._connect_twoshot(P_pad)  # collective
             if self.twoshot is None:
                 ub, pb, P_pad, lengths = plan_chunks(J, upp, W, self.nchunks_req)
+        hint = getattr(md, "engine_layout_hint", None)
+        if hint is not None:  # e.g. lanes grouped by forward path at the starting point
+            hint(guess)
         md.engine_set_chunks(ub)
         if self.size > 1 and dev.type == "cuda" and self.fuse_epilogue:
             from ..parallel.xgmi import get_oneshot
@@ -513,6 +527,28 @@ class FusedAdamEngine:
                 self.comm.all_reduce(dt, op="max")
             return float(dt) / n
 
+        from ..parallel.xgmi import CollectiveTimeout
+
+        def verdict(c):
+            """Collective: None if every rank's peer-memory exchanges of candidate ``c``
+            completed, else the reason (and the protocols are reset on every rank, so the
+            next candidate starts clean)."""
+            ctxs = [x for x in (self.twoshot, self.oneshot) if x is not None]
+            if not multi or not ctxs:
+                return None
+            flags = torch.zeros(self.size, dtype=torch.int64)
+            flags[self.rank] = int(any(int(x.err.item()) for x in ctxs))
+            self.comm.all_reduce(flags)
+            bad = [r for r in range(self.size) if int(flags[r])]
+            if not bad:
+                return None
+            for x in ctxs:
+                x.reset(self.comm)
+            return f"peer-memory exchange timed out on rank(s) {bad}"
+
+        cands = [dict(c) for c in cands]
+        dropped = []
+        self._fault_seen = set()
         self._tuning = True
         try:
             apply(cands[0])
@@ -521,20 +557,58 @@ class FusedAdamEngine:
             est = window(2)
             reps = int(min(max_reps, max(8, math.ceil(min_window_s / max(est, 1e-6)))))
             restore()
+            why = verdict(cands[0])
+            if why is not None:  # the probe of the first candidate already failed
+                dropped.append(dict(cands[0], reason=why))
             times = []
-            for c in cands:
+            for i, c in enumerate(cands):
+                if any(d.items() >= c.items() for d in dropped):
+                    times.append(math.inf)
+                    continue
                 apply(c)
+                self._fault_c = c
                 for _ in range(warm):
                     self._raw_step()
-                times.append(window(reps))
+                t = window(reps)
+                self._fault_c = None
                 restore()
+                why = verdict(c)
+                if why is not None:
+                    dropped.append(dict(c, reason=why))
+                    t = math.inf
+                times.append(t)
+            if all(math.isinf(t) for t in times) and self.twoshot is not None:
+                # no peer-memory schedule survived: the RCCL exchange on the same buffers
+                fb = {k: False for k in cands[0]}
+                fb["rccl_exchange"] = True
+                if fb in cands:
+                    times[cands.index(fb)] = math.inf
+                apply(fb)
+                for _ in range(warm):
+                    self._raw_step()
+                t = window(reps)
+                restore()
+                why = verdict(fb)
+                if why is not None:
+                    raise CollectiveTimeout(f"setup autotune: every exchange schedule failed ({why})")
+                if fb not in cands:
+                    cands.append(fb)
+                    times.append(t)
+                else:
+                    times[cands.index(fb)] = t
             self.check("setup autotune", collective=multi)
         finally:
             self._tuning = False
+            self._fault_c = None
+        if all(math.isinf(t) for t in times):
+            raise CollectiveTimeout(f"setup autotune: every candidate failed: {dropped}")
         best = min(range(len(cands)), key=lambda i: times[i])
         apply(cands[best])
-        self.tuning = {"candidates": [dict(c, ms=round(1e3 * t, 4)) for c, t in zip(cands, times)],
+        self.tuning = {"candidates": [dict(c, ms=round(1e3 * t, 4) if math.isfinite(t) else None)
+                                      for c, t in zip(cands, times)],
                        "chosen": cands[best], "steps_per_window": reps}
+        if dropped:
+            self.tuning["dropped"] = dropped
         if self.use_graph:
             # capture the real (trajectory-writing) step now rather than inside the first
             # timed step
@@ -583,6 +657,8 @@ class FusedAdamEngine:
         """Chunk c: dense-gradient reduce-scatter + Adam on the owned slice + all-gather,
         one launch on the side stream after the chunk's VJP."""
         side = self.ts_side
+        if self._inject_fault():
+            return  # test hook: this rank skips one exchange, so its peers time out
         if side:
             self.ev_vjp[c].record(torch.cuda.current_stream())
             self.comm_stream.wait_event(self.ev_vjp[c])
@@ -603,6 +679,26 @@ class FusedAdamEngine:
         if side:
             self.ev_ts[c].record(self.comm_stream)
             self._ts_pending[c] = True
+
+    def _inject_fault(self) -> bool:
+        """Test hook ``MULTIGRAD_AUTOTUNE_FAULT=<attr>=<0|1>:<rank>``: while the setup
+        autotune times a candidate with that attribute value, the given rank skips one
+        two-shot exchange (once per matching candidate and tuning), so its peers' exchange times
+        out (bounded wait) -- the way an exchange that fails on a real xGMI node shows up."""
+        spec = os.environ.get("MULTIGRAD_AUTOTUNE_FAULT")
+        c = getattr(self, "_fault_c", None)
+        if not spec or c is None:
+            return False
+        cond, _, rank = spec.partition(":")
+        key, _, val = cond.partition("=")
+        if key not in c or bool(c[key]) != (val.strip() == "1") or int(rank or 0) != self.rank:
+            return False
+        seen = self.__dict__.setdefault("_fault_seen", set())
+        ck = tuple(sorted(c.items()))
+        if ck in seen:
+            return False  # once per matching candidate
+        seen.add(ck)
+        return True
 
     def _owner_units(self, md, J):
         """Owner-mode unit bounds if the model's data placement allows it on every rank."""

@@ -74,6 +74,13 @@ class KeyNotCapturable(RuntimeError):
     """A hook used its randkey in a way a graph replay cannot reproduce."""
 
 
+class KeyAttributeNotCapturable(KeyNotCapturable, AttributeError):
+    """An attribute of the capture-time randkey other than ``generator``: also an
+    AttributeError, so ``hasattr(randkey, name)`` is False and ``getattr(randkey, name,
+    default)`` returns the default inside a captured step (a hook that only probes the key
+    stays capturable); using the attribute sends the run to the eager path."""
+
+
 class _CaptureKey:
     """The ``randkey`` the hooks see while a step is captured: only
     ``generator(<cuda device>)`` is allowed (graph-registered, seeded before each replay)."""
@@ -87,7 +94,9 @@ class _CaptureKey:
         return self._eng._next_generator(device)
 
     def __getattr__(self, name):
-        raise KeyNotCapturable(
+        if name.startswith("__") and name.endswith("__"):
+            raise AttributeError(name)  # protocol probes (copy, pickle, ...)
+        raise KeyAttributeNotCapturable(
             f"randkey.{name} inside a captured step: only randkey.generator(<cuda device>) "
             f"can be replayed with a fresh key per step")
 
@@ -217,7 +226,7 @@ class GraphAdamEngine:
                 q = 4 * W
                 P_pad = -(-P // q) * q
                 if sgd:  # the summed gradient itself is needed: a capturable all-reduce
-                    self.ar = get_twoshot_allreduce(self.comm, P)
+                    self.ar = get_twoshot_allreduce(self.comm, P, hold=True)
                 else:
                     self.twoshot = acquire_twoshot(self.comm, P_pad) if twoshot_enabled() else None
                 if self.group:
@@ -320,7 +329,11 @@ class GraphAdamEngine:
         if self.twoshot is not None:
             from ..parallel.xgmi import release_twoshot
             release_twoshot(self.comm, self.twoshot)
+        if self.ar is not None:
+            from ..parallel.xgmi import release_twoshot_allreduce
+            release_twoshot_allreduce(self.ar)
         self.twoshot = None
+        self.ar = None
         self.ready = False
 
     # ------------------------------------------------------------------ the step

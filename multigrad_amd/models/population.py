@@ -17,6 +17,8 @@ scaling: the total data is independent of the number of GPUs), on its own GPU.
 """
 from __future__ import annotations
 
+import math
+import os
 from dataclasses import dataclass
 from typing import Optional
 
@@ -88,7 +90,8 @@ def make_population_data(num_params: int = 10_000_000, num_halos: int = 1 << 27,
                          comm=None, device=None, nbins: int = 10, chunks: int = 1,
                          truth_offset=(0.1, 0.1), tail: str = "absolute",
                          layout: str = "auto", placement: str = "hashed",
-                         lane_order: Optional[str] = None) -> dict:
+                         lane_order: Optional[str] = None, narrow_frac: float = 0.0,
+                         narrow_log_sigma: float = -1.1) -> dict:
     """This rank's shard of the synthetic population-SMF data set.
 
     The global catalog (halo i: population ``hash(i) mod J``, log mass from a second hash)
@@ -116,6 +119,12 @@ def make_population_data(num_params: int = 10_000_000, num_halos: int = 1 << 27,
     the halos (profiles/hashed_proxy.md): tiles 94 + 63 us (forward + VJP), lanes with
     the local slot order and the recomputing VJP (``lane_order="local"``) 120 + 136 us,
     lanes global order with residuals 140 + 146 us.
+
+    ``narrow_frac``: the fraction of populations (chosen by a hash of the population id, so
+    scattered over the catalog) whose true log10 sigma is ``narrow_log_sigma`` (default
+    -1.1: sigma = 0.079 dex, a bin width of 1.26 sigma at the truth and 1.0 sigma at the
+    default guess), outside the Euler-Maclaurin forward's range of 0.5 sigma; these
+    populations take the per-edge path (profiles/narrow_sweep/).
 
     Returns a dict with the sorted device shard (``shard``), bins, volume, true
     parameters ``truth`` (interleaved, device) and a starting ``guess``; the target SMF is
@@ -160,6 +169,10 @@ def make_population_data(num_params: int = 10_000_000, num_halos: int = 1 << 27,
     truth = torch.empty(2 * npop, dtype=torch.float32, device=device)
     truth[0::2] = (-2.0 + 0.2 * (hash_uniform(cidx, seed + 2) - 0.5)).to(torch.float32)
     truth[1::2] = (-0.5 + 0.2 * (hash_uniform(cidx, seed + 3) - 0.5)).to(torch.float32)
+    if narrow_frac > 0:
+        narrow = hash_uniform(cidx, seed + 4) < float(narrow_frac)
+        truth[1::2] = torch.where(narrow, torch.full_like(truth[1::2], float(narrow_log_sigma)),
+                                  truth[1::2])
     guess = truth.clone()
     guess[0::2] += truth_offset[0]
     guess[1::2] += truth_offset[1]
@@ -229,6 +242,38 @@ class PopulationSMFModel(OnePointModel):
 
     def engine_set_chunks(self, unit_bounds):
         self.shard.set_chunks(unit_bounds)
+
+    def lane_fallback_groups(self, params) -> tuple:
+        """``(groups on the per-edge path, groups)`` of the lanes forward at ``params``
+        (user order): a group leaves the Euler-Maclaurin path when any of its lanes has a bin
+        width above 0.5 sigma.  (0, 0) for other layouts."""
+        sh = self.shard
+        d = self.bins.delta
+        if sh.layout != "lanes" or sh.device.type != "cuda" or d <= 0:
+            return 0, 0
+        s = torch.as_tensor(params, device=sh.device).reshape(-1)[1::2].float()
+        narrow = (s < math.log10(2.0 * d)).to(torch.int32)
+        sp = sh.slot_pop.long()
+        per_slot = torch.where(sp >= 0, narrow[sp.clamp(min=0)], torch.zeros_like(narrow[:1]))
+        g = per_slot.reshape(-1, 64).amax(1)
+        return int(g.sum()), int(g.numel())
+
+    def engine_layout_hint(self, guess) -> None:
+        """Group the lanes by forward path at the starting parameters (called by the fused
+        engine before :meth:`engine_set_chunks`): populations whose bin width exceeds the
+        Euler-Maclaurin range (h = delta / sigma > 0.5, csrc/smf.hip kEmHMax) get lane groups
+        of their own, so a few narrow populations do not send whole groups to the per-edge
+        path.  ``MULTIGRAD_LANE_CLASSES=0`` turns it off."""
+        sh = self.shard
+        if sh.layout != "lanes" or os.environ.get("MULTIGRAD_LANE_CLASSES", "1") == "0":
+            return
+        d = self.bins.delta
+        if d <= 0 or self.bins.rel_tail:
+            return
+        g = torch.as_tensor(guess).reshape(-1)
+        s = g[1::2].detach().to("cpu", torch.float64)
+        # h = delta / 10^s > 0.5  <=>  s < log10(2 delta)
+        sh.set_lane_classes((s < math.log10(2.0 * d)).to(torch.int64))
 
     def engine_owner_units(self):
         """Population (unit) bounds ``[W+1]`` of the owner placement, or None."""

@@ -58,6 +58,16 @@ class SmfBins:
         return self.tail == "relative"
 
     @property
+    def delta(self) -> float:
+        """Edge spacing when the edges are uniformly spaced (the Euler-Maclaurin forward's
+        condition, csrc/smf.hip make_bins), else 0."""
+        e = np.asarray(self.edges, dtype=np.float64)
+        d = (e[-1] - e[0]) / max(len(e) - 1, 1)
+        ok = d > 0 and np.all(np.abs(e - (e[0] + d * np.arange(len(e)))) <=
+                              1e-6 * np.maximum(1.0, np.abs(e)))
+        return float(d) if ok else 0.0
+
+    @property
     def nb(self) -> int:
         return len(self.scale)
 
@@ -178,6 +188,7 @@ class PopulationShard:
         # the lanes population order must be identical on every rank of a data-parallel
         # job: it is decided by the cross-rank sums of the counts
         self.order_counts = None
+        self.lane_class = None  # optional per-population class that groups lanes first
         if self.layout == "lanes" and lane_order == "global" and comm is not None and comm.size > 1:
             oc = counts.clone().to(torch.int64)
             comm.all_reduce(oc)
@@ -217,14 +228,40 @@ class PopulationShard:
         self.partials = torch.zeros(max(self.nslots, 1) * 2, dtype=torch.float32,
                                     device=self.device)
 
+    def set_lane_classes(self, cls: Optional[torch.Tensor]) -> bool:
+        """Per-population class (int, CPU or device, [npop]) that orders the slots of a
+        lanes window before the halo count: populations of one class share 64-lane groups.
+        The Euler-Maclaurin forward takes a group's fast path only when every lane's bin
+        width is inside its range, so the narrow populations of a fit (bin width > 0.5
+        sigma) are kept out of the other groups -- at 1% narrow populations in random
+        places, 47% of the groups would otherwise hold one.  Takes effect at the next
+        :meth:`set_chunks`; the class must be the same on every rank.  Returns whether it
+        changed."""
+        if cls is not None:
+            cls = torch.as_tensor(cls).reshape(-1).to("cpu", torch.int64)
+            assert cls.numel() == self.npop
+            if not bool((cls != 0).any()):
+                cls = None
+        old = self.lane_class
+        self.lane_class = cls
+        return not ((old is None and cls is None) or
+                    (old is not None and cls is not None and torch.equal(old, cls)))
+
+    def _order_key(self):
+        key = self.order_counts
+        if self.lane_class is None:
+            return key
+        base = self.counts.to(torch.int64) if key is None else key
+        return base + (self.lane_class << 40)
+
     def _build_lanes(self, pb) -> None:
         from ._schedule import build_lanes_py
+        key = self._order_key()
         try:
             out = ext().build_lanes(self.counts.to(torch.int64), list(pb[1:-1]),
-                                    self._lane_window, self._lane_lmax, self.order_counts)
+                                    self._lane_window, self._lane_lmax, key)
         except ImportError:
-            out = build_lanes_py(self.counts, pb[1:-1], self._lane_window, self._lane_lmax,
-                                 self.order_counts)
+            out = build_lanes_py(self.counts, pb[1:-1], self._lane_window, self._lane_lmax, key)
         (slot_pop, slot_src, slot_len, slot_part, group_base, group_len, chunk_groups, giant,
          chunk_giant, fwd_order, slot_pidx, perm) = out
         dev = self.device
@@ -322,7 +359,7 @@ class PopulationShard:
         plus, for residual forwards of the lanes layout, the fix-up launch's rows."""
         n = self.fwd_blocks(nhalos, nbins, log_sigma, rel_tail, chunk)
         if self.device.type == "cuda" and self.layout == "lanes" and resid:
-            n += LANES_FIX_BLOCKS
+            n += lanes_fix_blocks()
         return n
 
     @property
@@ -377,10 +414,20 @@ class PopulationShard:
 
 _GRID_CACHE: dict = {}
 # workgroups of the fix-up launch that evaluates the groups a residual lanes forward deferred
-# (outside the Euler-Maclaurin range; none in the headline data).  An empty fix-up launch of
-# 64 workgroups measured 16.5 us, of 1 workgroup 7.4 us (the count read and the reset are
-# memory round trips; the 64 tickets serialise): 8 keeps 32 waves for data that defers
+# (outside the Euler-Maclaurin range) in builds with -DMG_LANES_DEFER=1 (round 3).  An empty
+# fix-up launch of 64 workgroups measured 16.5 us, of 1 workgroup 7.4 us (the count read and
+# the reset are memory round trips; the 64 tickets serialise).  The default build
+# (MG_LANES_DEFER 2) evaluates those groups inside the main launch and has no fix-up rows.
 LANES_FIX_BLOCKS = int(os.environ.get("MULTIGRAD_FIX_BLOCKS", "8"))
+
+
+def lanes_fix_blocks() -> int:
+    """Slab rows of the fix-up launch of a residual lanes forward: LANES_FIX_BLOCKS when
+    the extension runs the deferral list (MG_LANES_DEFER 1), else 0."""
+    if "fix" not in _GRID_CACHE:
+        fn = getattr(ext(), "smf_lanes_fallback_mode", None)
+        _GRID_CACHE["fix"] = LANES_FIX_BLOCKS if fn is None or int(fn()) == 1 else 0
+    return _GRID_CACHE["fix"]
 
 
 def _sort_by_population(pop_cpu: torch.Tensor, npop: int):
@@ -497,8 +544,8 @@ def smf_forward_slab(theta: torch.Tensor, shard: PopulationShard, bins: SmfBins,
                                        shard.group_len, shard.fwd_order, theta, list(bins.edges),
                                        list(bins.scale), bool(log_sigma), g0, g1, slab, nblk,
                                        bins.rel_tail, rbuf, w_order, w_start, queues, upd, usc,
-                                       shard.defer_buffer() if resid else None,
-                                       LANES_FIX_BLOCKS if resid else 0, et, es, ep)
+                                       shard.defer_buffer() if resid and lanes_fix_blocks() else None,
+                                       lanes_fix_blocks() if resid else 0, et, es, ep)
         if resid:
             shard.resid_epoch += 1
         return int(rows)

@@ -36,7 +36,7 @@ import torch
 __all__ = ["OneShotAllReduce", "CollectiveTimeout", "oneshot_enabled", "oneshot_mode",
            "connect", "get_oneshot", "maybe_oneshot", "MAX_FLOATS", "MAX_RANKS", "TwoShot",
            "connect_twoshot", "twoshot_enabled", "get_twoshot_allreduce", "acquire_twoshot",
-           "release_twoshot", "status", "STRESS_REPS"]
+           "release_twoshot", "release_twoshot_allreduce", "status", "STRESS_REPS"]
 
 MAX_FLOATS = 64
 MAX_RANKS = 8
@@ -309,6 +309,11 @@ class TwoShot:
         self.seq = torch.zeros(1, dtype=torch.int32, device=dev)
         self.err = torch.zeros(1, dtype=torch.int32, device=dev)
         self._step0 = torch.zeros(2, dtype=torch.int32, device=dev)
+        # users of a cached all-reduce context (get_twoshot_allreduce): engines that hold it
+        # between calls, and graphs captured around it (pinned: a replay may come any time);
+        # the cache evicts only contexts that nobody holds
+        self.holders = 0
+        self.pinned = False
 
     def slice(self, rank: Optional[int] = None):
         """Owned float range ``(lo, n)`` of ``rank`` (default: this rank)."""
@@ -324,6 +329,9 @@ class TwoShot:
         gradients (self-test); 1: unbounded Adam; 2/3: bounded (3: legacy Jacobian).
         ``max_blocks`` caps the grid (0: the default 1024)."""
         from ..ops._ext import ext
+        if not self.regions:
+            raise RuntimeError("two-shot context used after close() (its peer memory is "
+                               "unmapped)")
         lo_b = hi_b = kind = None
         if bounds is not None:
             lo_b, hi_b, kind = bounds.lo, bounds.hi, bounds.kind
@@ -351,6 +359,8 @@ class TwoShot:
             raise ValueError("two-shot all_reduce_: contiguous fp32 tensor of at most "
                              f"{self.numel} elements expected, got {t.dtype} x {k}")
         flat = t.view(-1)
+        if torch.cuda.is_current_stream_capturing():
+            self.pinned = True  # a replay of this graph may come at any time: never evict
         self.grad[:k].copy_(flat)
         lo, n = self.slice()
         self.step(lo, n, 0)
@@ -426,7 +436,7 @@ class TwoShot:
 _MAX_AR_CONTEXTS = 4
 
 
-def get_twoshot_allreduce(comm, numel: int) -> Optional[TwoShot]:
+def get_twoshot_allreduce(comm, numel: int, hold: bool = False) -> Optional[TwoShot]:
     """A cached two-shot context able to sum ``numel`` fp32 values over ``comm`` (for
     capturable user-level all-reduces, :func:`multigrad_amd.ingraph.reduce_sum`);
     collective on first use for a given size class.  None when disabled or unavailable
@@ -435,8 +445,12 @@ def get_twoshot_allreduce(comm, numel: int) -> Optional[TwoShot]:
     The smallest cached context that is large enough is reused.  Connecting is
     collective and synchronises the host, so it is refused while a graph is being
     captured (connect before capturing: call once eagerly with the same size).  At most
-    ``_MAX_AR_CONTEXTS`` working contexts are kept; connecting a larger one closes the
-    smallest (every rank makes the same calls in the same order, so the caches agree)."""
+    ``_MAX_AR_CONTEXTS`` working contexts that nobody uses are kept; connecting a larger one
+    closes the smallest of those (every rank makes the same calls in the same order, so the
+    caches agree).  A context is in use while a caller holds it (``hold=True``, given back
+    with :func:`release_twoshot_allreduce`) or once a graph captured an exchange on it
+    (pinned for the communicator's lifetime: the graph may be replayed at any time); a
+    closed context raises on use instead of touching unmapped peer memory."""
     if (comm is None or comm.size < 2 or comm.size > MAX_RANKS or not twoshot_enabled()
             or not torch.cuda.is_available()):
         return None
@@ -447,7 +461,9 @@ def get_twoshot_allreduce(comm, numel: int) -> Optional[TwoShot]:
         cache = comm._twoshot_ar = {}
     fits = sorted(have for have, ts in cache.items() if ts and have >= want)
     if fits:
-        return cache[fits[0]]
+        ts = cache[fits[0]]
+        ts.holders += int(hold)
+        return ts
     if any(not ts and have <= want for have, ts in cache.items()):
         return None  # a failed connect at this size or below: the peers are unusable
     if torch.cuda.is_current_stream_capturing():
@@ -457,13 +473,21 @@ def get_twoshot_allreduce(comm, numel: int) -> Optional[TwoShot]:
             f"cannot contain; run one eager call of this size on every rank first")
     ts = connect_twoshot(comm, want, _timeout_s()) or False
     cache[want] = ts
-    live = sorted(have for have, t in cache.items() if t)
-    while len(live) > _MAX_AR_CONTEXTS:
+    if ts:
+        ts.holders += int(hold)
+    idle = sorted(have for have, t in cache.items() if t and not t.holders and not t.pinned)
+    while len(idle) > _MAX_AR_CONTEXTS:
         torch.cuda.synchronize()
         comm.barrier()
-        cache.pop(live[0]).close()
-        live.pop(0)
+        cache.pop(idle[0]).close()
+        idle.pop(0)
     return ts or None
+
+
+def release_twoshot_allreduce(ts: Optional[TwoShot]) -> None:
+    """Give back a context taken with ``get_twoshot_allreduce(..., hold=True)``."""
+    if ts:
+        ts.holders = max(0, ts.holders - 1)
 
 
 def acquire_twoshot(comm, numel: int) -> Optional[TwoShot]:

@@ -133,7 +133,9 @@ def load_optimizer_state(path: str, map_location="cpu", rank: Optional[int] = No
     st, err = None, None
     try:
         st = _load_shard(path, r, map_location)
-    except (CheckpointMismatch, OSError, RuntimeError, ValueError) as exc:
+    except Exception as exc:  # noqa: BLE001 -- every failure must reach the collective
+        # verdict (an unpickling error, EOFError of a truncated file, KeyError of a broken
+        # manifest ...): a rank that raised here alone would leave its peers in allgather
         err = f"{type(exc).__name__}: {exc}"
     if comm is not None and comm.size > 1:
         errs = comm.allgather(err)

@@ -167,6 +167,36 @@ def test_sharded_checkpoint_manifest(tmp_path):
     assert man == {"step": 7, "size": 2, "sharded": True, "shards": "opt.pt.step7.rank{rank}"}
 
 
+def _ckpt_broken_body(rank, size, path, kind):
+    import pickle
+    comm = mg.get_world_comm()
+    ckpt.save_optimizer_state(path, {"step": 3, "size": size, "x": torch.ones(2)},
+                              comm=comm, sharded=True)
+    comm.barrier()
+    if rank == 1:
+        fn = ckpt.shard_path(path, 1, 3)
+        if kind == "empty":  # truncated to zero bytes (EOFError / RuntimeError in torch.load)
+            open(fn, "wb").close()
+        else:  # a plain pickle of a non-weights object: weights_only refuses it
+            with open(fn, "wb") as f:
+                pickle.dump(_ckpt_broken_body, f)
+    comm.barrier()
+    try:
+        ckpt.load_optimizer_state(path, rank=rank, sharded=True, comm=comm)
+        return "loaded"
+    except ckpt.CheckpointMismatch as e:
+        return "rank(s) [1]" in str(e)
+
+
+@pytest.mark.parametrize("kind", ["empty", "pickle"])
+def test_sharded_checkpoint_broken_shard_raises_everywhere(tmp_path, kind):
+    """Any failure of one rank's shard load (not only the anticipated exception types)
+    reaches the collective verdict: every rank raises instead of the healthy ones hanging."""
+    path = str(tmp_path / "opt.pt")
+    res = run_distributed(_ckpt_broken_body, 2, path, kind, timeout=120)
+    assert res == [True, True], res
+
+
 # ------------------------------------------------------------------ two "nodes"
 def _nodes_body(rank, size):
     os.environ["MULTIGRAD_NODE_NAME"] = "nodeB" if rank % 2 else "nodeA"

@@ -153,3 +153,18 @@ def test_generic_engine_group_matches_eager_group():
         np.testing.assert_allclose(t, tr, rtol=1e-5, atol=1e-6)
     for r in range(1, 4):
         np.testing.assert_array_equal(eng[r][0], eng[0][0])
+
+
+def test_capture_key_attribute_probes_are_attribute_errors():
+    """hasattr / getattr-with-default on the capture-time randkey behave like on
+    any object without that attribute; using the attribute raises KeyNotCapturable (which
+    sends the engine to the eager path)."""
+    from multigrad_amd.engine.generic import KeyNotCapturable, _CaptureKey
+    k = _CaptureKey(eng=None)
+    assert not hasattr(k, "split")
+    assert getattr(k, "seed", 7) == 7
+    with pytest.raises(KeyNotCapturable):
+        k.split(2)
+    import copy
+    with pytest.raises(Exception):
+        copy.copy(k).split  # protocol probes fall through to plain AttributeErrors

@@ -377,10 +377,11 @@ def test_fused_epilogue_matches_separate_kernels(graph):
 
 @pytest.mark.parametrize("narrow", [False, True])
 def test_folded_epilogue_matches_separate_launch(monkeypatch, narrow):
-    """The sumstat epilogue folded into the single-workgroup fix-up launch of the deferred
-    lanes groups (MULTIGRAD_FOLD_EPILOGUE) against the separate epilogue launch, pipelined,
-    with no group deferred and with narrow populations that the fix-up must evaluate; the
-    deferral list is left at zero after every step."""
+    """The sumstat epilogue passed to the forward's launch sequence
+    (MULTIGRAD_FOLD_EPILOGUE: with the default MG_LANES_DEFER 2 build the forward launches
+    it right after the main kernel; with -DMG_LANES_DEFER=1 it rides on the fix-up launch)
+    against the engine's own epilogue launch, pipelined, with no narrow population and
+    with narrow populations on the per-edge path; the deferral list stays at zero."""
     from multigrad_amd.engine.fused import FusedAdamEngine
     from multigrad_amd.models.population import PopulationSMFModel, make_population_data
     data = make_population_data(num_params=6000, num_halos=300_000, seed=21, device=DEV)
@@ -549,8 +550,8 @@ def test_em_forward_fallback_groups_vs_fp64():
     th = _narrow_guess(data)
     out = torch.zeros(bins.nbp, device=DEV)
     S.smf_forward_into(th, shard, bins, True, out, resid=True)
-    # the narrow groups went through the deferral list and the fix-up launch, which leaves
-    # the list's counters at zero for the next launch
+    # the narrow groups went through the out-of-line per-edge call (default build) or the
+    # deferral list and fix-up launch (-DMG_LANES_DEFER=1), which leaves the counters at 0
     assert int(shard.defer_buffer()[:2].abs().sum()) == 0
     ref = S.smf_sumstats_reference(th.double(), shard.x.double(), shard.pop, bins, True)
     np.testing.assert_allclose(out[:bins.nb].cpu().double(), ref.cpu(), rtol=2e-5)
@@ -588,7 +589,7 @@ def test_pipelined_update_with_fallback_groups_matches_unpipelined(monkeypatch):
 
 
 def test_headline_kernel_vs_fp64(monkeypatch):
-    """The exact timed instantiation -- smf_fwd_lanes_kernel<10,true,false,true,true,1>, the
+    """The exact timed instantiation -- smf_fwd_lanes_kernel<10,true,false,true,true,3>, the
     pipelined forward with the fused VJP + Adam, at the headline size (1e7 parameters,
     1.34e8 halos) -- for 2 steps: S(theta_1) against the fp64 oracle (rtol 2e-5), and the
     step-0 gradient (read back from the first Adam moment, m = (1 - b1) g) on 2000

@@ -112,3 +112,36 @@ def test_internal_order_is_rank_independent():
     p0 = build_lanes_py(l0, [1000], 256, 4096, glob)[-1]
     p1 = build_lanes_py(l1, [1000], 256, 4096, glob)[-1]
     assert torch.equal(p0, p1)
+
+
+def test_lane_classes_group_narrow_populations():
+    """PopulationShard.set_lane_classes: populations of one class share 64-lane groups, so
+    1% narrow populations scattered over the catalog put about 1% of the groups (plus at
+    most one mixed group per window) on the per-edge path instead of ~47% (every group with
+    one narrow lane).  The order inside a class stays by halo count."""
+    from multigrad_amd.models.population import make_population_data
+    data = make_population_data(num_params=2 * 20_000, num_halos=540_000, seed=3, device="cpu")
+    sh = data["shard"]
+    rng = np.random.default_rng(1)
+    cls = torch.tensor(rng.random(sh.npop) < 0.01, dtype=torch.int64)
+
+    def mixed_and_narrow():
+        sp = sh.slot_pop.long()
+        c = torch.where(sp >= 0, cls[sp.clamp(min=0)], torch.zeros(1, dtype=torch.int64))
+        g = c.reshape(-1, 64)
+        occupied = (sp.reshape(-1, 64) >= 0)
+        narrow = g.amax(1) > 0
+        mixed = narrow & ((g == 0) & occupied).any(1)
+        return int(narrow.sum()), int(mixed.sum()), g.shape[0]
+
+    n0, _, G = mixed_and_narrow()
+    assert n0 > 0.3 * G  # without classes: a large share of groups hold a narrow lane
+    assert sh.set_lane_classes(cls)
+    assert not sh.set_lane_classes(cls)  # unchanged
+    sh.set_chunks(sh.chunk_pops)
+    n1, mixed, G1 = mixed_and_narrow()
+    windows = -(-sh.npop // sh._lane_window)
+    assert mixed <= windows and n1 <= int(cls.sum()) // 64 + 2 * windows, (n1, mixed, windows)
+    assert sh.set_lane_classes(None)
+    sh.set_chunks(sh.chunk_pops)
+    assert mixed_and_narrow()[0] == n0
