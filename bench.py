@@ -148,10 +148,8 @@ def time_placement(placement, args, comm, dev, sync):
                  learning_rate=args.lr, history=history)
     sync()
     setup_s = time.perf_counter() - t_setup
-    fb = model.lane_fallback_groups(data["guess"])
 
-    for _ in range(args.warmup):
-        engine.step()
+    engine.steps(args.warmup)
     # the last warmup step's pending (pipelined) update is applied before the clock starts,
     # so the timed region holds exactly K forwards and K updates (the K-th one in drain())
     engine.drain()
@@ -160,14 +158,14 @@ def time_placement(placement, args, comm, dev, sync):
     comm.barrier()
     sync()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        engine.step()
+    engine.steps(args.steps)  # graph mode: blocks of engine.graph_steps steps per replay
     engine.drain()  # the pipelined last update / last all-gathers are inside the timing
     sync()
     comm.barrier()
     elapsed = time.perf_counter() - t0
     engine.check()  # a failed peer exchange raises here instead of reporting wrong numbers
     loss1 = engine.last_loss()
+    fb = model.lane_fallback_groups(data["guess"])  # lane groups on the per-edge path
     ops = {}
     if count:  # after the timing: device operations of one steady-state step
         from multigrad_amd.utils.profiling import count_device_ops
@@ -184,6 +182,7 @@ def time_placement(placement, args, comm, dev, sync):
         "ms_per_step": 1e3 * elapsed / args.steps,
         "parallelism": f"dp{comm.size}" + ("-owner" if engine.owner else ""),
         "graph": bool(engine.use_graph),
+        "graph_steps": int(engine.graph_steps) if engine.use_graph else 0,
         "pipelined": bool(engine.pipeline),
         "optimizer_sharding": ("owner" if engine.owner else "zero1" if engine.zero
                                else "replicated"),
@@ -296,6 +295,7 @@ def main(argv=None):
             "optimizer": "Adam (fused HIP kernel), full trajectory" if history == "full"
                          else f"Adam (fused HIP kernel), history={history}",
             "graph": head["graph"],
+            "graph_steps": head["graph_steps"],
             "pipelined": head["pipelined"],
             "optimizer_sharding": head["optimizer_sharding"],
             "placement": head["placement"],

@@ -2,6 +2,7 @@
 #include <torch/extension.h>
 
 #include <tuple>
+#include <string>
 #include <vector>
 
 namespace mg {
@@ -10,7 +11,8 @@ int smf_padded_bins(int64_t nb);
 int64_t smf_fwd_max_blocks(int64_t nb, bool log_sigma, bool has_pop, bool rel_tail);
 void smf_forward(torch::Tensor x, c10::optional<torch::Tensor> pop, torch::Tensor theta,
                  std::vector<double> edges, std::vector<double> scale, bool log_sigma,
-                 int64_t begin, int64_t end, torch::Tensor slab, int64_t nblocks, bool rel_tail);
+                 int64_t begin, int64_t end, torch::Tensor slab, int64_t nblocks, bool rel_tail,
+                 std::string exchange);
 void smf_slab_reduce(torch::Tensor slab, int64_t nrows, std::vector<double> edges,
                      std::vector<double> scale, torch::Tensor out);
 void smf_edge_weights(torch::Tensor g, std::vector<double> edges, std::vector<double> scale,
@@ -21,7 +23,8 @@ void smf_logmse(torch::Tensor S, torch::Tensor target, double eps, std::vector<d
 void smf_vjp(torch::Tensor x, c10::optional<torch::Tensor> pop, torch::Tensor theta,
              torch::Tensor tiles, int64_t tile_begin, int64_t tile_end, torch::Tensor h,
              std::vector<double> edges, std::vector<double> scale, bool log_sigma,
-             torch::Tensor grad, torch::Tensor partials, torch::Tensor giant);
+             torch::Tensor grad, torch::Tensor partials, torch::Tensor giant,
+             std::string exchange);
 int64_t smf_fwd_lanes_max_blocks(int64_t nb, bool log_sigma, bool rel_tail, bool resid);
 int64_t smf_lanes_fallback_mode();
 void smf_lanes_pack(torch::Tensor xs, torch::Tensor slot_src, torch::Tensor slot_len,
@@ -39,7 +42,7 @@ int64_t smf_forward_lanes(torch::Tensor xi, torch::Tensor slot_pop, torch::Tenso
                        std::vector<double> update_scalars,
                        c10::optional<torch::Tensor> defer, int64_t fix_blocks,
                        std::vector<torch::Tensor> epi_tensors, std::vector<double> epi_scalars,
-                       std::vector<int64_t> epi_peers);
+                       std::vector<int64_t> epi_peers, bool per_edge);
 void smf_vjp_lanes(torch::Tensor slot_pop, torch::Tensor slot_part, torch::Tensor theta,
                    torch::Tensor h, torch::Tensor resid, int64_t s0, int64_t s1,
                    std::vector<double> scale, bool log_sigma, torch::Tensor grad,
@@ -71,6 +74,15 @@ void xgmi_twoshot(std::vector<int64_t> gbufs, std::vector<int64_t> tbufs, std::v
                   c10::optional<torch::Tensor> bhi, c10::optional<torch::Tensor> kind,
                   c10::optional<torch::Tensor> traj, torch::Tensor step, torch::Tensor seq,
                   torch::Tensor err, std::vector<double> scalars);
+pybind11::bytes xgmi_twoshot_pack(std::vector<int64_t> gbufs, std::vector<int64_t> tbufs,
+                                  std::vector<int64_t> flags, int64_t rank, int64_t lo, int64_t n,
+                                  int64_t total, int64_t mode, c10::optional<torch::Tensor> u,
+                                  c10::optional<torch::Tensor> m, c10::optional<torch::Tensor> v,
+                                  c10::optional<torch::Tensor> blo, c10::optional<torch::Tensor> bhi,
+                                  c10::optional<torch::Tensor> kind, c10::optional<torch::Tensor> traj,
+                                  torch::Tensor step, torch::Tensor seq, torch::Tensor err,
+                                  std::vector<double> scalars);
+void xgmi_twoshot_launch_packed(std::string packed);
 int64_t xgmi_twoshot_flag_bytes();
 pybind11::bytes xgmi_handle(int64_t base);
 int64_t xgmi_open(pybind11::bytes handle);
@@ -120,12 +132,20 @@ PYBIND11_MODULE(_C, m) {
     return d;
   });
   m.def("smf_padded_bins", &mg::smf_padded_bins);
-  m.def("smf_forward", &mg::smf_forward);
+  m.def("smf_forward", &mg::smf_forward, pybind11::arg("x"), pybind11::arg("pop"),
+        pybind11::arg("theta"), pybind11::arg("edges"), pybind11::arg("scale"),
+        pybind11::arg("log_sigma"), pybind11::arg("begin"), pybind11::arg("end"),
+        pybind11::arg("slab"), pybind11::arg("nblocks"), pybind11::arg("rel_tail"),
+        pybind11::arg("exchange") = std::string());
   m.def("smf_fwd_max_blocks", &mg::smf_fwd_max_blocks);
   m.def("smf_slab_reduce", &mg::smf_slab_reduce);
   m.def("smf_edge_weights", &mg::smf_edge_weights);
   m.def("smf_logmse", &mg::smf_logmse);
-  m.def("smf_vjp", &mg::smf_vjp);
+  m.def("smf_vjp", &mg::smf_vjp, pybind11::arg("x"), pybind11::arg("pop"), pybind11::arg("theta"),
+        pybind11::arg("tiles"), pybind11::arg("tile_begin"), pybind11::arg("tile_end"),
+        pybind11::arg("h"), pybind11::arg("edges"), pybind11::arg("scale"),
+        pybind11::arg("log_sigma"), pybind11::arg("grad"), pybind11::arg("partials"),
+        pybind11::arg("giant"), pybind11::arg("exchange") = std::string());
   m.def("smf_fwd_lanes_max_blocks", &mg::smf_fwd_lanes_max_blocks);
   m.def("smf_lanes_pack", &mg::smf_lanes_pack);
   m.def("smf_lanes_fallback_mode", &mg::smf_lanes_fallback_mode);
@@ -140,7 +160,7 @@ PYBIND11_MODULE(_C, m) {
         pybind11::arg("defer") = pybind11::none(), pybind11::arg("fix_blocks") = 0,
         pybind11::arg("epi_tensors") = std::vector<torch::Tensor>(),
         pybind11::arg("epi_scalars") = std::vector<double>(),
-        pybind11::arg("epi_peers") = std::vector<int64_t>());
+        pybind11::arg("epi_peers") = std::vector<int64_t>(), pybind11::arg("per_edge") = false);
   m.def("lpt_waves", &mg::lpt_waves);
   m.def("smf_vjp_lanes", &mg::smf_vjp_lanes);
   m.def("smf_vjp_adam_lanes", &mg::smf_vjp_adam_lanes);
@@ -154,6 +174,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("xgmi_alloc", &mg::xgmi_alloc, pybind11::arg("bytes") = 0);
   m.def("xgmi_tensor", &mg::xgmi_tensor);
   m.def("xgmi_twoshot", &mg::xgmi_twoshot);
+  m.def("xgmi_twoshot_pack", &mg::xgmi_twoshot_pack);
+  m.def("xgmi_twoshot_launch_packed", &mg::xgmi_twoshot_launch_packed);
   m.def("xgmi_twoshot_flag_bytes", &mg::xgmi_twoshot_flag_bytes);
   m.def("xgmi_handle", &mg::xgmi_handle);
   m.def("xgmi_open", &mg::xgmi_open);

@@ -22,6 +22,7 @@
 // sums are combined in a fixed order by a finalize kernel (this is also the path of the
 // 2-parameter shared-parameter models).
 #include "common.h"
+#include "twoshot.h"
 #include "xgmi.h"
 #include "tail_table.h"
 
@@ -203,11 +204,23 @@ constexpr int kFwdUnroll = MG_FWD_UNROLL;
 #define MG_FWD_PIPE 1
 #endif
 
-template <int NB, bool LOGSIG, bool HAS_POP, bool REL>
+// XS (fused exchange): workgroups [0, xs.blocks) run the two-shot exchange of the previous
+// parameter chunk (twoshot.h) and the rest this forward, with their own block numbering --
+// the exchange overlaps the forward without a second stream or cross-stream events.
+template <int NB, bool LOGSIG, bool HAS_POP, bool REL, bool XS = false>
 __global__ __launch_bounds__(kThreads, MG_FWD_MINWAVES) void smf_fwd_kernel(
     const float* __restrict__ x, const int32_t* __restrict__ pop,
     const float2* __restrict__ theta, int64_t begin, int64_t end, SmfBins bins,
-    float* __restrict__ slab) {
+    float* __restrict__ slab, TwoShotPack xs = TwoShotPack{}) {
+  int bid = blockIdx.x, nblk = gridDim.x;
+  if constexpr (XS) {
+    if (bid < xs.blocks) {
+      twoshot_block_fused(xs.a, bid, xs.blocks);
+      return;
+    }
+    bid -= xs.blocks;
+    nblk -= xs.blocks;
+  }
   // signed-tail table: 8 replicas (8 workgroups per CU share the LDS)
   constexpr int kRepl = (!REL && MG_FWD_TAB >= 1 && MG_FWD_BALLOT) ? 8 : 0;
   const float4* tb = nullptr;
@@ -224,7 +237,7 @@ __global__ __launch_bounds__(kThreads, MG_FWD_MINWAVES) void smf_fwd_kernel(
 #pragma unroll
   for (int k = 0; k <= NB; ++k) cnt[k] = 0;
   const float2 th0 = HAS_POP ? make_float2(0.f, 0.f) : theta[0];
-  const int64_t stride = (int64_t)gridDim.x * kThreads;
+  const int64_t stride = (int64_t)nblk * kThreads;
   // the loop is wave-uniform (trip count from the wave's first halo; lanes past the end
   // are masked with x = -inf), so the ballot counts stay in SGPRs and are complete
   const int lane = threadIdx.x & (kWave - 1);
@@ -245,7 +258,7 @@ __global__ __launch_bounds__(kThreads, MG_FWD_MINWAVES) void smf_fwd_kernel(
         ps[u] = ok ? pop[i] : 0;
       }
     };
-    int64_t w0 = begin + (int64_t)blockIdx.x * kThreads + wbase;
+    int64_t w0 = begin + (int64_t)bid * kThreads + wbase;
     float xa[kFwdUnroll], xb[kFwdUnroll];
     int pa[kFwdUnroll], pb[kFwdUnroll];
     float2 tha[kFwdUnroll];
@@ -273,7 +286,7 @@ __global__ __launch_bounds__(kThreads, MG_FWD_MINWAVES) void smf_fwd_kernel(
     }
   } else
 #endif
-  for (int64_t w0 = begin + (int64_t)blockIdx.x * kThreads + wbase; w0 < end;
+  for (int64_t w0 = begin + (int64_t)bid * kThreads + wbase; w0 < end;
        w0 += kFwdUnroll * stride) {
     // issue every load of this iteration before any math (one dependent round trip)
     float xs[kFwdUnroll];
@@ -305,7 +318,7 @@ __global__ __launch_bounds__(kThreads, MG_FWD_MINWAVES) void smf_fwd_kernel(
   block_sum_n<NB>(bin, scratch);
   if (threadIdx.x == 0) {
 #pragma unroll
-    for (int k = 0; k < NB; ++k) slab[(int64_t)blockIdx.x * NB + k] = acc[k];
+    for (int k = 0; k < NB; ++k) slab[(int64_t)bid * NB + k] = acc[k];
   }
 }
 
@@ -1163,7 +1176,7 @@ __device__ __forceinline__ void halo_vjp_rec(float nm, float inv, float dw, cons
   wc = ws.x;
 }
 
-template <int NB, bool LOGSIG>
+template <int NB, bool LOGSIG, bool XS = false>
 #ifndef MG_VJP_REC_MINWAVES
 #define MG_VJP_REC_MINWAVES 8  // 20 KB of LDS and <= 64 VGPRs: 8 workgroups per CU
 #endif
@@ -1171,13 +1184,24 @@ __global__ __launch_bounds__(kThreads, MG_VJP_REC_MINWAVES) void smf_vjp_tiles_r
     const float* __restrict__ x, const int32_t* __restrict__ pop,
     const float2* __restrict__ theta, const Tile* __restrict__ tiles,
     const float* __restrict__ hvec, SmfBins bins, float2* __restrict__ grad,
-    float2* __restrict__ partials) {
+    float2* __restrict__ partials, TwoShotPack xs = TwoShotPack{}) {
+  // XS (fused exchange): workgroups [0, xs.blocks) run the two-shot exchange of the
+  // previous parameter chunk (its gradient is complete: the launch that wrote it ended
+  // before this one), the rest one tile each
+  int tb = blockIdx.x;
+  if constexpr (XS) {
+    if (tb < xs.blocks) {
+      twoshot_block_fused(xs.a, tb, xs.blocks);
+      return;
+    }
+    tb -= xs.blocks;
+  }
   using EP = EdgePairs<NB>;
   constexpr int M = EP::NP / 2;
   // LDS (20 KB, so 8 workgroups fit a CU): per-halo contributions (later the per-population
   // results) and local population ids (later the head partials and their successors)
   __shared__ __attribute__((aligned(16))) char smem[kTileHalos * (sizeof(float2) + sizeof(int16_t))];
-  const Tile t = tiles[blockIdx.x];
+  const Tile t = tiles[tb];
   const int tid = threadIdx.x;
   if (t.slot >= 0) {  // partial tile (one giant population): the per-edge block reduction
     float h[NB + 1];
@@ -1576,7 +1600,8 @@ __global__ __launch_bounds__(kThreads, MG_LANES_MINWAVES) void smf_fwd_lanes_ker
     const int32_t* __restrict__ wave_start, int* __restrict__ queues, int nq,
     LanesUpdate upd = LanesUpdate{}, int* __restrict__ defer = nullptr, EpiArgs epi = EpiArgs{}) {
   static_assert(!UPD || RESID, "the pipelined update reads the residuals it overwrites");
-  static_assert(LMODE == 0 || (RESID && MG_FWD_EM && MG_LANES_EP && !REL), "deferral: EM residual forwards");
+  static_assert(LMODE == 0 || LMODE == 4 || (RESID && MG_FWD_EM && MG_LANES_EP && !REL),
+                "deferral: EM residual forwards");
   static_assert(LMODE != 2 || !UPD, "the fix-up launch evaluates updated groups");
   if constexpr (LMODE == 2) {  // the listed groups, grid-strided
     fwd_order = defer + 2;
@@ -1585,10 +1610,14 @@ __global__ __launch_bounds__(kThreads, MG_LANES_MINWAVES) void smf_fwd_lanes_ker
   }
   // signed-tail table (absolute contract): 16 replicas (conflict-free reads), 8 next to
   // the pipelined update's staging buffer (LDS budget of 4 workgroups per CU)
+  // LMODE 4 (PER-EDGE): no Euler-Maclaurin path; every group by the packed two-halo
+  // per-edge tails (the kernel of builds with MG_FWD_EM=0), for shards where most lane
+  // groups are outside the EM range anyway
+  constexpr bool kEmOn = MG_FWD_EM && LMODE != 4;
   constexpr int kRepl =
-      (!REL && MG_LANES_EP && !(MG_FWD_EM) && (MG_FWD_TAB >= 2 || (MG_FWD_TAB == 1 && !RESID)))
-          ? (UPD ? 8 : 16) : 0;  // (with MG_FWD_EM the fallback is the lean per-edge path)
-  constexpr bool kEm = MG_FWD_EM && MG_LANES_EP && !REL;
+      (!REL && MG_LANES_EP && !kEmOn && (MG_FWD_TAB >= 2 || (MG_FWD_TAB == 1 && !RESID)))
+          ? (UPD ? 8 : 16) : 0;  // (with the EM path the fallback is the lean per-edge path)
+  constexpr bool kEm = kEmOn && MG_LANES_EP && !REL;
   const float4* tb = nullptr;
   if constexpr (kRepl > 0) {
     __shared__ float4 tab[kTailTabN * (kRepl > 0 ? kRepl : 1)];
@@ -2254,9 +2283,13 @@ int64_t smf_fwd_max_blocks(int64_t nb, bool log_sigma, bool has_pop, bool rel_ta
 }
 
 // Forward over halos [begin, end); writes slab[nblocks * NBP].
+// exchange (bytes of xgmi_twoshot_pack, or empty): a two-shot exchange this launch runs in
+// extra leading workgroups (fused exchange); kernels that cannot carry it (no population
+// ids, relative tails) launch it on its own first.
 void smf_forward(torch::Tensor x, c10::optional<torch::Tensor> pop, torch::Tensor theta,
                  std::vector<double> edges, std::vector<double> scale, bool log_sigma,
-                 int64_t begin, int64_t end, torch::Tensor slab, int64_t nblocks, bool rel_tail) {
+                 int64_t begin, int64_t end, torch::Tensor slab, int64_t nblocks, bool rel_tail,
+                 std::string exchange) {
   check_dev(x, "x", at::kFloat);
   check_dev(theta, "theta", at::kFloat);
   check_dev(slab, "slab", at::kFloat);
@@ -2277,10 +2310,26 @@ void smf_forward(torch::Tensor x, c10::optional<torch::Tensor> pop, torch::Tenso
   const int32_t* pp = has_pop ? pop->data_ptr<int32_t>() : nullptr;
   const float2* tp = reinterpret_cast<const float2*>(theta.data_ptr<float>());
   float* sp = slab.data_ptr<float>();
+  if (!exchange.empty()) {
+    const TwoShotPack xs = twoshot_unpack(exchange);
+    if (has_pop && !rel_tail && xs.mode == 1) {
+      TORCH_CHECK(nblocks + xs.blocks <= 65535, "bad block count");
+      MG_DISPATCH_NB(nbp, {
+        with_bool(log_sigma, [&](auto LS) {
+          hipLaunchKernelGGL((smf_fwd_kernel<NB, decltype(LS)::value, true, false, true>),
+                             dim3(nblocks + xs.blocks), dim3(kThreads), 0, stream, xp, pp, tp, begin,
+                             end, b, sp, xs);
+        });
+      });
+      return;
+    }
+    twoshot_launch(xs, stream);
+  }
   MG_DISPATCH_NB(nbp, {
     with_bool(log_sigma, [&](auto LS) { with_bool(has_pop, [&](auto HP) { with_bool(rel_tail, [&](auto RT) {
       hipLaunchKernelGGL((smf_fwd_kernel<NB, decltype(LS)::value, decltype(HP)::value, decltype(RT)::value>),
-                         dim3(nblocks), dim3(kThreads), 0, stream, xp, pp, tp, begin, end, b, sp);
+                         dim3(nblocks), dim3(kThreads), 0, stream, xp, pp, tp, begin, end, b, sp,
+                         TwoShotPack{});
     }); }); });
   });
 }
@@ -2398,10 +2447,13 @@ void smf_epilogue(torch::Tensor slab, int64_t nrows, std::vector<double> edges,
 }
 
 // VJP over a tile schedule; grad is interleaved [2 * npop]; partials [nslots * 2].
+// exchange: as in smf_forward (the recurrence kernel carries it; the others launch it on
+// its own first).
 void smf_vjp(torch::Tensor x, c10::optional<torch::Tensor> pop, torch::Tensor theta,
              torch::Tensor tiles, int64_t tile_begin, int64_t tile_end, torch::Tensor h,
              std::vector<double> edges, std::vector<double> scale, bool log_sigma,
-             torch::Tensor grad, torch::Tensor partials, torch::Tensor giant) {
+             torch::Tensor grad, torch::Tensor partials, torch::Tensor giant,
+             std::string exchange) {
   check_dev(x, "x", at::kFloat);
   check_dev(theta, "theta", at::kFloat);
   check_dev(h, "h", at::kFloat);
@@ -2425,7 +2477,23 @@ void smf_vjp(torch::Tensor x, c10::optional<torch::Tensor> pop, torch::Tensor th
   float2* pa = partials.numel() ? reinterpret_cast<float2*>(partials.data_ptr<float>()) : nullptr;
   // the recurrence kernel needs uniform, unpadded bins (b.delta > 0) and population ids
   const bool rec = MG_VJP_REC && b.delta > 0.0f && has_pop;
-  if (ntiles > 0) {
+  bool fused = false;
+  if (!exchange.empty()) {
+    const TwoShotPack xs = twoshot_unpack(exchange);
+    if (rec && xs.mode == 1) {
+      TORCH_CHECK(ntiles + xs.blocks <= INT32_MAX, "bad block count");
+      MG_DISPATCH_NB(nbp, {
+        if (log_sigma)
+          hipLaunchKernelGGL((smf_vjp_tiles_rec_kernel<NB, true, true>), dim3(ntiles + xs.blocks), dim3(kThreads), 0, stream, xp, pp, tp, tl, h.data_ptr<float>(), b, gp, pa, xs);
+        else
+          hipLaunchKernelGGL((smf_vjp_tiles_rec_kernel<NB, false, true>), dim3(ntiles + xs.blocks), dim3(kThreads), 0, stream, xp, pp, tp, tl, h.data_ptr<float>(), b, gp, pa, xs);
+      });
+      fused = true;
+    } else {
+      twoshot_launch(xs, stream);
+    }
+  }
+  if (ntiles > 0 && !fused) {
     MG_DISPATCH_NB(nbp, {
       if (rec) {
         if (log_sigma)
@@ -2584,7 +2652,7 @@ int64_t smf_forward_lanes(torch::Tensor xi, torch::Tensor slot_pop, torch::Tenso
                        std::vector<double> update_scalars,
                        c10::optional<torch::Tensor> defer, int64_t fix_blocks,
                        std::vector<torch::Tensor> epi_tensors, std::vector<double> epi_scalars,
-                       std::vector<int64_t> epi_peers) {
+                       std::vector<int64_t> epi_peers, bool per_edge) {
   check_dev(xi, "xi", at::kFloat);
   check_dev(slot_pop, "slot_pop", at::kInt);
   check_dev(group_base, "group_base", at::kLong);
@@ -2651,8 +2719,11 @@ int64_t smf_forward_lanes(torch::Tensor xi, torch::Tensor slot_pop, torch::Tenso
   // the Euler-Maclaurin residual forwards: out-of-range groups through the out-of-line call
   // (LMODE 3, MG_LANES_DEFER 2) or the deferral list (LMODE 1 + 2, MG_LANES_DEFER 1)
   const bool em_resid = has_resid && MG_FWD_EM && MG_LANES_EP && !rel_tail && b.delta > 0.0f;
-  const bool lmode = dp != nullptr && MG_LANES_DEFER == 1 && em_resid;
-  const bool lcall = MG_LANES_DEFER == 2 && em_resid;
+  // per_edge (the caller's choice when most groups are outside the EM range, e.g. a fit
+  // with narrow populations everywhere): LMODE 4, the per-edge kernel for every group
+  const bool ledge = per_edge && em_resid && MG_LANES_EP;
+  const bool lmode = !ledge && dp != nullptr && MG_LANES_DEFER == 1 && em_resid;
+  const bool lcall = !ledge && MG_LANES_DEFER == 2 && em_resid;
   // Sumstat epilogue folded into this launch sequence (epi_tensors = [slab of all chunks,
   // target, S, loss, h, seq, err, advance] (empty = absent), epi_scalars = [rows before this
   // chunk, eps, rank, timeout_s], epi_peers): the fix-up launch becomes one workgroup that
@@ -2736,6 +2807,12 @@ int64_t smf_forward_lanes(torch::Tensor xi, torch::Tensor slot_pop, torch::Tenso
                              slot_pop.data_ptr<int32_t>(), group_base.data_ptr<int64_t>(),
                              group_len.data_ptr<int32_t>(), order, tp, g0, g1, b,
                              slab.data_ptr<float>(), rp, ws, qp, nq, u, dp);
+        } else if (ledge) {
+          hipLaunchKernelGGL((smf_fwd_lanes_kernel<NB, decltype(LS)::value, false, true, true, 4>),
+                             dim3(nblocks), dim3(kThreads), 0, stream, xi.data_ptr<float>(),
+                             slot_pop.data_ptr<int32_t>(), group_base.data_ptr<int64_t>(),
+                             group_len.data_ptr<int32_t>(), order, tp, g0, g1, b,
+                             slab.data_ptr<float>(), rp, ws, qp, nq, u);
         } else {
           with_bool(rel_tail, [&](auto RT) {
             hipLaunchKernelGGL((smf_fwd_lanes_kernel<NB, decltype(LS)::value, decltype(RT)::value, true, true>),
@@ -2760,6 +2837,12 @@ int64_t smf_forward_lanes(torch::Tensor xi, torch::Tensor slot_pop, torch::Tenso
                            slot_pop.data_ptr<int32_t>(), group_base.data_ptr<int64_t>(),
                            group_len.data_ptr<int32_t>(), order, tp, g0, g1, b,
                            slab.data_ptr<float>(), rp, ws, qp, nq, LanesUpdate{}, dp);
+      } else if (ledge) {
+        hipLaunchKernelGGL((smf_fwd_lanes_kernel<NB, decltype(LS)::value, false, true, false, 4>),
+                           dim3(nblocks), dim3(kThreads), 0, stream, xi.data_ptr<float>(),
+                           slot_pop.data_ptr<int32_t>(), group_base.data_ptr<int64_t>(),
+                           group_len.data_ptr<int32_t>(), order, tp, g0, g1, b,
+                           slab.data_ptr<float>(), rp, ws, qp, nq);
       } else {
         with_bool(rel_tail, [&](auto RT) { with_bool(has_resid, [&](auto RS) {
           hipLaunchKernelGGL((smf_fwd_lanes_kernel<NB, decltype(LS)::value, decltype(RT)::value, decltype(RS)::value>),

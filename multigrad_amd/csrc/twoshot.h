@@ -1,0 +1,173 @@
+// Two-shot reduce-scatter -> Adam -> all-gather over peer memory (see xgmi.hip for the
+// protocol), as the work of a range of workgroups: the stand-alone exchange kernel
+// (xgmi.hip) and the compute kernels that run the exchange of the previous parameter chunk
+// in their first workgroups (smf.hip, "fused exchange": the exchange of chunk c-1 overlaps
+// the VJP of chunk c without a second stream or cross-stream events).
+#pragma once
+
+#include "adam.h"
+#include "common.h"
+#include "xgmi.h"
+
+#include <cstring>
+#include <stdexcept>
+#include <string>
+
+namespace mg {
+
+struct TwoShotArgs {
+  XgmiPeers g;          // peers' gradient regions (as mapped in this process)
+  XgmiPeers t;          // peers' parameter regions
+  XgmiPeers f;          // peers' flag regions
+  int rank, size;
+  int64_t lo, n;        // owned float range; lo % 4 == 0, n % 4 == 0
+  float* u;             // bounded: owned u slice; unbounded: nullptr (u = own parameters)
+  float* m;
+  float* v;
+  const float* blo;     // owned bounds (bounded modes)
+  const float* bhi;
+  const int8_t* kind;
+  float* traj;          // owned trajectory base (row r at traj + r * traj_stride) or null
+  int64_t traj_stride;
+  int* step;            // device step counter [step, ticket] (read when host_step < 0)
+  int host_step;
+  unsigned* seq;
+  int* err;
+  long long ticks;
+  float lr, b1, b2, eps;
+};
+
+constexpr int kTsThreads = 256;
+
+// MODE 0: plain sum (self-test: theta = sum of the gradients); 1: Adam, unbounded;
+// 2: Adam in bounded coordinates; 3: bounded with the reference's legacy Jacobian (Q1).
+// The exchange as workgroups [0, nblk) of the calling grid (bid = this workgroup's index in
+// that range).  Every workgroup of the range must call it; it returns when this
+// workgroup's share is done (the last one returns when every rank's slice has landed).
+template <int MODE, int PB = kXMaxRanks>
+__device__ __forceinline__ void twoshot_block(const TwoShotArgs& a, int bid, int nblk) {
+  static_assert(kXMaxRanks % PB == 0, "peer batches must tile the rank limit");
+  constexpr bool BOUNDED = MODE >= 2;
+  constexpr bool LEGACY = MODE == 3;
+  const unsigned seq = __hip_atomic_load(a.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+  const int st = a.host_step >= 0
+                     ? a.host_step
+                     : __hip_atomic_load(a.step, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  char* me = a.f.base[a.rank];
+  // my gradient is complete: the VJP's stores to the uncached buffer were acknowledged
+  // before that launch ended, and this launch is ordered after it
+  if (bid == 0 && (int)threadIdx.x < a.size) uc_signal(ts_gflag(a.f.base[threadIdx.x]) + a.rank, seq);
+  const int bad = ts_wait_all(ts_gflag(me), a.size, seq, a.err, a.ticks);
+  const float bc1 = 1.0f - powf(a.b1, (float)(st + 1));
+  const float bc2 = 1.0f - powf(a.b2, (float)(st + 1));
+  float* trow = a.traj ? a.traj + (int64_t)(st + 1) * a.traj_stride : nullptr;
+  const float* own = reinterpret_cast<const float*>(a.t.base[a.rank]) + a.lo;
+  const int64_t n4 = a.n >> 2;
+  const int64_t stride = (int64_t)nblk * kTsThreads;
+  for (int64_t i = (int64_t)bid * kTsThreads + threadIdx.x; i < n4; i += stride) {
+    const int64_t off = a.lo + 4 * i;
+    // the peers' loads are issued PB at a time before their adds (the peer loop is unrolled
+    // to the compile-time rank limit), so PB remote round trips overlap instead of running
+    // one after another; the sum is taken in rank order either way (same bits for any PB).
+    // PB = 8: every load in flight (the stand-alone kernel); PB = 4 keeps the registers of
+    // the compute kernels that carry the exchange (fused exchange)
+    float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int q0 = 0; q0 < kXMaxRanks; q0 += PB) {
+      float4 hs[PB];
+#pragma unroll
+      for (int j = 0; j < PB; ++j)
+        if (q0 + j < a.size)
+          hs[j] = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(a.g.base[q0 + j]) + off);
+#pragma unroll
+      for (int j = 0; j < PB; ++j) {
+        if (q0 + j == 0) {
+          g = hs[0];
+        } else if (q0 + j < a.size) {
+          g.x += hs[j].x; g.y += hs[j].y; g.z += hs[j].z; g.w += hs[j].w;
+        }
+      }
+    }
+    float4 p = g;
+    if constexpr (MODE >= 1) {
+      float4 u = BOUNDED ? reinterpret_cast<const float4*>(a.u)[i]
+                         : reinterpret_cast<const float4*>(own)[i];
+      float4 m = reinterpret_cast<const float4*>(a.m)[i];
+      float4 v = reinterpret_cast<const float4*>(a.v)[i];
+      float4 po = make_float4(0.f, 0.f, 0.f, 0.f), lo = po, hi = po;
+      char4 k = make_char4(0, 0, 0, 0);
+      if constexpr (BOUNDED) {
+        lo = reinterpret_cast<const float4*>(a.blo)[i];
+        hi = reinterpret_cast<const float4*>(a.bhi)[i];
+        k = reinterpret_cast<const char4*>(a.kind)[i];
+        if (LEGACY) po = reinterpret_cast<const float4*>(own)[i];
+      }
+      adam_elem<BOUNDED, LEGACY>(a, bc1, bc2, g.x, u.x, m.x, v.x, po.x, lo.x, hi.x, k.x, p.x);
+      adam_elem<BOUNDED, LEGACY>(a, bc1, bc2, g.y, u.y, m.y, v.y, po.y, lo.y, hi.y, k.y, p.y);
+      adam_elem<BOUNDED, LEGACY>(a, bc1, bc2, g.z, u.z, m.z, v.z, po.z, lo.z, hi.z, k.z, p.z);
+      adam_elem<BOUNDED, LEGACY>(a, bc1, bc2, g.w, u.w, m.w, v.w, po.w, lo.w, hi.w, k.w, p.w);
+      if (bad) {
+        const float nan = __builtin_nanf("");
+        u = make_float4(nan, nan, nan, nan);
+        p = u;
+      }
+      reinterpret_cast<float4*>(a.m)[i] = m;
+      reinterpret_cast<float4*>(a.v)[i] = v;
+      if constexpr (BOUNDED) reinterpret_cast<float4*>(a.u)[i] = u;
+      if (trow) reinterpret_cast<float4*>(trow)[i] = p;
+    } else if (bad) {
+      const float nan = __builtin_nanf("");
+      p = make_float4(nan, nan, nan, nan);
+    }
+    for (int q = 0; q < a.size; ++q)
+      *reinterpret_cast<float4*>(reinterpret_cast<float*>(a.t.base[q]) + off) = p;
+  }
+  // grid completion: every thread's pushes are acknowledged before its block takes a
+  // ticket; the last block publishes "my slice is everywhere" and waits until every
+  // peer's slice has landed here
+  uc_release();
+  __syncthreads();
+  __shared__ int last;
+  if (threadIdx.x == 0) {
+    const unsigned tk = atomicAdd(ts_ticket(me), 1u);
+    last = tk == (unsigned)nblk - 1;
+  }
+  __syncthreads();
+  if (!last) return;
+  if (threadIdx.x == 0) __hip_atomic_store(ts_ticket(me), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if ((int)threadIdx.x < a.size) uc_signal(ts_tflag(a.f.base[threadIdx.x]) + a.rank, seq);
+  ts_wait_all(ts_tflag(me), a.size, seq, a.err, a.ticks);
+  if (threadIdx.x == 0) {
+    __hip_atomic_store(a.seq, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (a.host_step < 0) __hip_atomic_store(a.step, st + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+
+// The exchange carried by a compute kernel (fused exchange): unbounded Adam only (the
+// bounded modes launch on their own, see smf_forward / smf_vjp), peers 4 at a time.
+__device__ __forceinline__ void twoshot_block_fused(const TwoShotArgs& a, int bid, int nblk) {
+  twoshot_block<1, 4>(a, bid, nblk);
+}
+
+// Packed launch arguments of one exchange (xgmi_twoshot_pack -> the fused kernels' host
+// wrappers): the struct, the mode and the workgroup count, as raw bytes.
+struct TwoShotPack {
+  TwoShotArgs a;
+  int mode;
+  int blocks;
+};
+
+// Stand-alone launch of a packed exchange on `stream` (xgmi.hip): the fallback of the
+// compute launches that cannot carry it (e.g. non-uniform bins in the VJP).
+void twoshot_launch(const TwoShotPack& P, hipStream_t stream);
+
+// The packed exchange from the bytes of xgmi_twoshot_pack (host side).
+inline TwoShotPack twoshot_unpack(const std::string& b) {
+  TwoShotPack P;
+  if (b.size() != sizeof(P)) throw std::runtime_error("bad packed two-shot exchange");
+  std::memcpy(&P, b.data(), sizeof(P));
+  return P;
+}
+
+}  // namespace mg

@@ -24,6 +24,7 @@
 // processes sharing one GPU (tests/test_xgmi_gpu.py).
 #include "adam.h"
 #include "common.h"
+#include "twoshot.h"
 #include "xgmi.h"
 
 #include <torch/extension.h>
@@ -145,121 +146,9 @@ void xgmi_allreduce(torch::Tensor x, std::vector<int64_t> peers, int64_t rank, t
 // overwrite its gradient (next VJP) while a peer still reads it.  The sequence number
 // lives in device memory (graph replayable); bounded waits raise err and NaN-poison the
 // owned slice instead of hanging.
-struct TwoShotArgs {
-  XgmiPeers g;          // peers' gradient regions (as mapped in this process)
-  XgmiPeers t;          // peers' parameter regions
-  XgmiPeers f;          // peers' flag regions
-  int rank, size;
-  int64_t lo, n;        // owned float range; lo % 4 == 0, n % 4 == 0
-  float* u;             // bounded: owned u slice; unbounded: nullptr (u = own parameters)
-  float* m;
-  float* v;
-  const float* blo;     // owned bounds (bounded modes)
-  const float* bhi;
-  const int8_t* kind;
-  float* traj;          // owned trajectory base (row r at traj + r * traj_stride) or null
-  int64_t traj_stride;
-  int* step;            // device step counter [step, ticket] (read when host_step < 0)
-  int host_step;
-  unsigned* seq;
-  int* err;
-  long long ticks;
-  float lr, b1, b2, eps;
-};
-
-constexpr int kTsThreads = 256;
-
-// MODE 0: plain sum (self-test: theta = sum of the gradients); 1: Adam, unbounded;
-// 2: Adam in bounded coordinates; 3: bounded with the reference's legacy Jacobian (Q1).
 template <int MODE>
 __global__ __launch_bounds__(kTsThreads) void xgmi_twoshot_kernel(TwoShotArgs a) {
-  constexpr bool BOUNDED = MODE >= 2;
-  constexpr bool LEGACY = MODE == 3;
-  const unsigned seq = __hip_atomic_load(a.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
-  const int st = a.host_step >= 0
-                     ? a.host_step
-                     : __hip_atomic_load(a.step, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  char* me = a.f.base[a.rank];
-  // my gradient is complete: the VJP's stores to the uncached buffer were acknowledged
-  // before that launch ended, and this launch is ordered after it
-  if (blockIdx.x == 0 && (int)threadIdx.x < a.size) uc_signal(ts_gflag(a.f.base[threadIdx.x]) + a.rank, seq);
-  const int bad = ts_wait_all(ts_gflag(me), a.size, seq, a.err, a.ticks);
-  const float bc1 = 1.0f - powf(a.b1, (float)(st + 1));
-  const float bc2 = 1.0f - powf(a.b2, (float)(st + 1));
-  float* trow = a.traj ? a.traj + (int64_t)(st + 1) * a.traj_stride : nullptr;
-  const float* own = reinterpret_cast<const float*>(a.t.base[a.rank]) + a.lo;
-  const int64_t n4 = a.n >> 2;
-  const int64_t stride = (int64_t)gridDim.x * kTsThreads;
-  for (int64_t i = (int64_t)blockIdx.x * kTsThreads + threadIdx.x; i < n4; i += stride) {
-    const int64_t off = a.lo + 4 * i;
-    // every peer's load is issued before the first add (the peer loop is unrolled to the
-    // compile-time rank limit), so the W remote round trips overlap instead of running one
-    // after another; the sum is still taken in rank order
-    float4 hs[kXMaxRanks];
-#pragma unroll
-    for (int q = 0; q < kXMaxRanks; ++q)
-      if (q < a.size)
-        hs[q] = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(a.g.base[q]) + off);
-    float4 g = hs[0];
-#pragma unroll
-    for (int q = 1; q < kXMaxRanks; ++q) {
-      if (q < a.size) {
-        g.x += hs[q].x; g.y += hs[q].y; g.z += hs[q].z; g.w += hs[q].w;
-      }
-    }
-    float4 p = g;
-    if constexpr (MODE >= 1) {
-      float4 u = BOUNDED ? reinterpret_cast<const float4*>(a.u)[i]
-                         : reinterpret_cast<const float4*>(own)[i];
-      float4 m = reinterpret_cast<const float4*>(a.m)[i];
-      float4 v = reinterpret_cast<const float4*>(a.v)[i];
-      float4 po = make_float4(0.f, 0.f, 0.f, 0.f), lo = po, hi = po;
-      char4 k = make_char4(0, 0, 0, 0);
-      if constexpr (BOUNDED) {
-        lo = reinterpret_cast<const float4*>(a.blo)[i];
-        hi = reinterpret_cast<const float4*>(a.bhi)[i];
-        k = reinterpret_cast<const char4*>(a.kind)[i];
-        if (LEGACY) po = reinterpret_cast<const float4*>(own)[i];
-      }
-      adam_elem<BOUNDED, LEGACY>(a, bc1, bc2, g.x, u.x, m.x, v.x, po.x, lo.x, hi.x, k.x, p.x);
-      adam_elem<BOUNDED, LEGACY>(a, bc1, bc2, g.y, u.y, m.y, v.y, po.y, lo.y, hi.y, k.y, p.y);
-      adam_elem<BOUNDED, LEGACY>(a, bc1, bc2, g.z, u.z, m.z, v.z, po.z, lo.z, hi.z, k.z, p.z);
-      adam_elem<BOUNDED, LEGACY>(a, bc1, bc2, g.w, u.w, m.w, v.w, po.w, lo.w, hi.w, k.w, p.w);
-      if (bad) {
-        const float nan = __builtin_nanf("");
-        u = make_float4(nan, nan, nan, nan);
-        p = u;
-      }
-      reinterpret_cast<float4*>(a.m)[i] = m;
-      reinterpret_cast<float4*>(a.v)[i] = v;
-      if constexpr (BOUNDED) reinterpret_cast<float4*>(a.u)[i] = u;
-      if (trow) reinterpret_cast<float4*>(trow)[i] = p;
-    } else if (bad) {
-      const float nan = __builtin_nanf("");
-      p = make_float4(nan, nan, nan, nan);
-    }
-    for (int q = 0; q < a.size; ++q)
-      *reinterpret_cast<float4*>(reinterpret_cast<float*>(a.t.base[q]) + off) = p;
-  }
-  // grid completion: every thread's pushes are acknowledged before its block takes a
-  // ticket; the last block publishes "my slice is everywhere" and waits until every
-  // peer's slice has landed here
-  uc_release();
-  __syncthreads();
-  __shared__ int last;
-  if (threadIdx.x == 0) {
-    const unsigned tk = atomicAdd(ts_ticket(me), 1u);
-    last = tk == gridDim.x - 1;
-  }
-  __syncthreads();
-  if (!last) return;
-  if (threadIdx.x == 0) __hip_atomic_store(ts_ticket(me), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if ((int)threadIdx.x < a.size) uc_signal(ts_tflag(a.f.base[threadIdx.x]) + a.rank, seq);
-  ts_wait_all(ts_tflag(me), a.size, seq, a.err, a.ticks);
-  if (threadIdx.x == 0) {
-    __hip_atomic_store(a.seq, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (a.host_step < 0) __hip_atomic_store(a.step, st + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
+  twoshot_block<MODE>(a, blockIdx.x, gridDim.x);
 }
 
 static XgmiPeers peers_of(const std::vector<int64_t>& v) {
@@ -277,15 +166,17 @@ static float* opt_ptr(const c10::optional<torch::Tensor>& t, int64_t numel, cons
   return t->data_ptr<float>();
 }
 
-// One two-shot step (see above).  mode: 0 sum, 1 Adam, 2 bounded Adam, 3 bounded legacy.
-// scalars: [host_step, lr, b1, b2, eps, timeout_s, traj_stride]
-void xgmi_twoshot(std::vector<int64_t> gbufs, std::vector<int64_t> tbufs, std::vector<int64_t> flags,
-                  int64_t rank, int64_t lo, int64_t n, int64_t total, int64_t mode,
-                  c10::optional<torch::Tensor> u, c10::optional<torch::Tensor> m,
-                  c10::optional<torch::Tensor> v, c10::optional<torch::Tensor> blo,
-                  c10::optional<torch::Tensor> bhi, c10::optional<torch::Tensor> kind,
-                  c10::optional<torch::Tensor> traj, torch::Tensor step, torch::Tensor seq,
-                  torch::Tensor err, std::vector<double> scalars) {
+// Launch arguments of one two-shot step (see above).  mode: 0 sum, 1 Adam, 2 bounded
+// Adam, 3 bounded legacy.  scalars: [host_step, lr, b1, b2, eps, timeout_s, traj_stride
+// (, max_blocks)]; returns the packed arguments with the mode and the workgroup count.
+static TwoShotPack twoshot_args(std::vector<int64_t> gbufs, std::vector<int64_t> tbufs,
+                                std::vector<int64_t> flags, int64_t rank, int64_t lo, int64_t n,
+                                int64_t total, int64_t mode, c10::optional<torch::Tensor> u,
+                                c10::optional<torch::Tensor> m, c10::optional<torch::Tensor> v,
+                                c10::optional<torch::Tensor> blo, c10::optional<torch::Tensor> bhi,
+                                c10::optional<torch::Tensor> kind, c10::optional<torch::Tensor> traj,
+                                torch::Tensor step, torch::Tensor seq, torch::Tensor err,
+                                std::vector<double> scalars) {
   const int size = (int)gbufs.size();
   TORCH_CHECK(size >= 1 && size <= kXMaxRanks && (int)tbufs.size() == size && (int)flags.size() == size,
               "two-shot: 1..8 ranks, one region of each kind per rank");
@@ -298,7 +189,8 @@ void xgmi_twoshot(std::vector<int64_t> gbufs, std::vector<int64_t> tbufs, std::v
   TORCH_CHECK(step.is_cuda() && step.scalar_type() == at::kInt && step.numel() >= 2, "step: [2] int32 device");
   TORCH_CHECK(seq.is_cuda() && seq.scalar_type() == at::kInt && err.is_cuda() && err.scalar_type() == at::kInt,
               "seq/err: int32 device");
-  TwoShotArgs a;
+  TwoShotPack P;
+  TwoShotArgs& a = P.a;
   a.g = peers_of(gbufs);
   a.t = peers_of(tbufs);
   a.f = peers_of(flags);
@@ -335,14 +227,54 @@ void xgmi_twoshot(std::vector<int64_t> gbufs, std::vector<int64_t> tbufs, std::v
   // grid cap: 1024 by default; a smaller cap (scalars[7]) leaves the CUs to the compute
   // kernels an exchange on a side stream overlaps (the grid-stride loop covers any size)
   const int64_t cap = scalars.size() == 8 && scalars[7] >= 1 ? std::min<int64_t>((int64_t)scalars[7], 1024) : 1024;
-  const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((n4 + kTsThreads - 1) / kTsThreads, cap));
-  auto stream = at::hip::getCurrentHIPStream();
-  switch (mode) {
-    case 0: hipLaunchKernelGGL(xgmi_twoshot_kernel<0>, dim3(blocks), dim3(kTsThreads), 0, stream, a); break;
-    case 1: hipLaunchKernelGGL(xgmi_twoshot_kernel<1>, dim3(blocks), dim3(kTsThreads), 0, stream, a); break;
-    case 2: hipLaunchKernelGGL(xgmi_twoshot_kernel<2>, dim3(blocks), dim3(kTsThreads), 0, stream, a); break;
-    default: hipLaunchKernelGGL(xgmi_twoshot_kernel<3>, dim3(blocks), dim3(kTsThreads), 0, stream, a); break;
+  P.mode = (int)mode;
+  P.blocks = (int)std::max<int64_t>(1, std::min<int64_t>((n4 + kTsThreads - 1) / kTsThreads, cap));
+  return P;
+}
+
+// One two-shot step (see above), launched on the current stream.
+void xgmi_twoshot(std::vector<int64_t> gbufs, std::vector<int64_t> tbufs, std::vector<int64_t> flags,
+                  int64_t rank, int64_t lo, int64_t n, int64_t total, int64_t mode,
+                  c10::optional<torch::Tensor> u, c10::optional<torch::Tensor> m,
+                  c10::optional<torch::Tensor> v, c10::optional<torch::Tensor> blo,
+                  c10::optional<torch::Tensor> bhi, c10::optional<torch::Tensor> kind,
+                  c10::optional<torch::Tensor> traj, torch::Tensor step, torch::Tensor seq,
+                  torch::Tensor err, std::vector<double> scalars) {
+  const TwoShotPack P = twoshot_args(gbufs, tbufs, flags, rank, lo, n, total, mode, u, m, v, blo,
+                                     bhi, kind, traj, step, seq, err, scalars);
+  twoshot_launch(P, at::hip::getCurrentHIPStream());
+}
+
+void twoshot_launch(const TwoShotPack& P, hipStream_t stream) {
+  switch (P.mode) {
+    case 0: hipLaunchKernelGGL(xgmi_twoshot_kernel<0>, dim3(P.blocks), dim3(kTsThreads), 0, stream, P.a); break;
+    case 1: hipLaunchKernelGGL(xgmi_twoshot_kernel<1>, dim3(P.blocks), dim3(kTsThreads), 0, stream, P.a); break;
+    case 2: hipLaunchKernelGGL(xgmi_twoshot_kernel<2>, dim3(P.blocks), dim3(kTsThreads), 0, stream, P.a); break;
+    default: hipLaunchKernelGGL(xgmi_twoshot_kernel<3>, dim3(P.blocks), dim3(kTsThreads), 0, stream, P.a); break;
   }
+}
+
+// A packed exchange launched on its own on the current stream (the last chunk's exchange
+// of a fused-exchange step when no further compute launch carries it).
+void xgmi_twoshot_launch_packed(std::string packed) {
+  twoshot_launch(twoshot_unpack(packed), at::hip::getCurrentHIPStream());
+}
+
+// The same step's arguments packed as bytes, for a compute launch that runs the exchange
+// in its first workgroups (smf.hip fused exchange: smf_forward / smf_vjp ``exchange``);
+// Adam modes only.  The tensors must stay alive until that launch is enqueued.
+pybind11::bytes xgmi_twoshot_pack(std::vector<int64_t> gbufs, std::vector<int64_t> tbufs,
+                                  std::vector<int64_t> flags, int64_t rank, int64_t lo, int64_t n,
+                                  int64_t total, int64_t mode, c10::optional<torch::Tensor> u,
+                                  c10::optional<torch::Tensor> m, c10::optional<torch::Tensor> v,
+                                  c10::optional<torch::Tensor> blo, c10::optional<torch::Tensor> bhi,
+                                  c10::optional<torch::Tensor> kind, c10::optional<torch::Tensor> traj,
+                                  torch::Tensor step, torch::Tensor seq, torch::Tensor err,
+                                  std::vector<double> scalars) {
+  TORCH_CHECK(mode >= 1, "a fused exchange is an Adam step (mode 1..3)");
+  const TwoShotPack P = twoshot_args(gbufs, tbufs, flags, rank, lo, n, total, mode, u, m, v, blo,
+                                     bhi, kind, traj, step, seq, err, scalars);
+  return pybind11::bytes(reinterpret_cast<const char*>(&P), sizeof(P));
 }
 
 int64_t xgmi_twoshot_flag_bytes() { return kTsFlagBytes; }

@@ -132,6 +132,18 @@ class FusedAdamEngine:
     it is requested -- the analogue of the reference's end-of-run trajectory broadcast.
     """
 
+    @property
+    def graph(self):
+        """The captured one-step graph (None: capture on first use).  Dropping it also
+        drops the graph of a block of steps."""
+        return self._graph
+
+    @graph.setter
+    def graph(self, g):
+        self._graph = g
+        if g is None:
+            self._kgraph = None
+
     def __init__(self, model, comm=None, graph: Optional[bool] = None,
                  zero: Optional[bool] = None, chunks: Optional[int] = None,
                  owner: Optional[bool] = None):
@@ -162,6 +174,13 @@ class FusedAdamEngine:
         g = _env_flag("MULTIGRAD_GRAPH", graph)
         self._graph_auto = g is None
         self.use_graph = (self.size == 1) if g is None else bool(g)
+        # whole-loop capture (the analogue of the reference's lax.scan over the optimizer
+        # loop, multigrad/mpi4jax/multigrad.py:57-58): graph mode replays graphs of
+        # graph_steps unrolled steps, so the ~10 us host launch and the ~10 us device gap
+        # between consecutive graph launches are paid once per block, not per step
+        # (profiles/graph_modes/); MULTIGRAD_GRAPH_STEPS, 1 = one step per graph
+        self.graph_steps = max(1, int(os.environ.get("MULTIGRAD_GRAPH_STEPS", "16")))
+        self._kgraph = None
         self.graph = None
         self._capturing = False
         self.pending = False
@@ -417,6 +436,22 @@ class FusedAdamEngine:
             self.ev_ts = [torch.cuda.Event() for _ in range(self.C)]
             self.ts_side = side_mode == "on"
         self._ts_pending = [False] * self.C
+        # fused exchange ("ts_fused"): the two-shot exchange of chunk c-1 runs in the first
+        # workgroups of chunk c's VJP launch and the last chunk's in the next step's first
+        # forward launch (csrc/twoshot.h) -- overlap with compute on ONE stream, no events.
+        # Unbounded fits with >= 2 chunks on a model whose kernels carry it.
+        # MULTIGRAD_TWOSHOT_FUSED: auto (an autotune candidate), on (always, no tuning), off
+        self._x_pending = None  # packed exchange of the last chunk, for the next launch
+        fmode = os.environ.get("MULTIGRAD_TWOSHOT_FUSED", "auto").strip().lower()
+        self.ts_fused_ok = bool(
+            fmode not in ("0", "off", "false", "no") and self.twoshot is not None
+            and self.C > 1 and bounds is None
+            and getattr(md, "engine_fused_exchange_ok", lambda: False)())
+        self.ts_fused = self.ts_fused_ok and fmode in ("1", "on", "true", "yes")
+        if self.ts_fused:
+            self.ts_side = False
+        if self.ts_fused_ok and not hasattr(self, "ts_blocks"):
+            self.ts_blocks = int(os.environ.get("MULTIGRAD_TWOSHOT_BLOCKS", "256"))
         self.pending = False
         ok = getattr(md, "engine_pipeline_ok", None)
         self.pipeline = bool(
@@ -427,12 +462,13 @@ class FusedAdamEngine:
         # a step can be captured when every collective in it is a peer-memory kernel with
         # its sequence number in device memory (one-shot sumstats, two-shot gradient) --
         # RCCL/gloo calls are not captured
-        self.capturable = dev.type == "cuda" and (
+        # (the fused exchange carries a step's last exchange into the next step: eager only)
+        self.capturable = dev.type == "cuda" and not self.ts_fused and (
             self.size == 1 or (self.oneshot is not None and self.fuse_epilogue and
                                (self.owner or (self.twoshot is not None and not self.ts_side))))
         if self._graph_auto:
             # a pipelined step is two launches (forward+update, epilogue); replaying them
-            # from a graph measured 1-5% slower than eager launches (tools/graph_ab_full.sh).
+            # from a graph measured 1-5% slower than eager launches (tools/archive/graph_ab_full.sh).
             # Multi-rank steps are capturable (MULTIGRAD_GRAPH=1, tested bitwise against
             # eager) but replays measured 7x slower than the 4 eager launches of the hashed
             # step with two ranks on one GPU (profiles/twoshot_2rank.md): eager by default.
@@ -451,16 +487,21 @@ class FusedAdamEngine:
             self.comm.barrier()
         cands = []
         if self.comm_stream is not None and side_mode == "auto" and not self.use_graph and \
-                xmode != "rccl":
+                xmode != "rccl" and not self.ts_fused:
             # hashed: where the exchange runs -- two-shot on the compute stream, on the side
             # stream, or RCCL's reduce-scatter / all-gather (measured, not assumed;
             # MULTIGRAD_HASHED_EXCHANGE=twoshot|rccl pins it)
-            cands = [{"ts_side": False, "rccl_exchange": False},
-                     {"ts_side": True, "rccl_exchange": False}]
+            cands = [{"ts_side": False, "rccl_exchange": False, "ts_fused": False},
+                     {"ts_side": True, "rccl_exchange": False, "ts_fused": False}]
+            if self.ts_fused_ok:
+                cands.append({"ts_side": False, "rccl_exchange": False, "ts_fused": True})
             if xmode != "twoshot":
-                cands.append({"ts_side": False, "rccl_exchange": True})
+                cands.append({"ts_side": False, "rccl_exchange": True, "ts_fused": False})
         elif self._graph_auto and self.capturable and (self.size == 1 or self.owner):
-            cands = [{"use_graph": False}, {"use_graph": True}]  # eager launches vs replay
+            # eager launches vs one-step replays vs replays of blocks of steps
+            cands = [{"use_graph": False}, {"use_graph": True, "graph_steps": 1}]
+            if self.graph_steps > 1 and (self.history.mode == "full" or self.traj_loc is not None):
+                cands.append({"use_graph": True, "graph_steps": self.graph_steps})
         if cands and dev.type == "cuda" and _env_flag("MULTIGRAD_AUTOTUNE", True) and \
                 not getattr(self, "_skip_autotune", False):
             self._autotune(cands, min_window_s=1e-3 * float(
@@ -518,8 +559,7 @@ class FusedAdamEngine:
             if multi:
                 self.comm.barrier()
             t0 = time.perf_counter()
-            for _ in range(n):
-                self._raw_step()
+            self._run_steps(n)
             self._drain_all()
             torch.cuda.synchronize()
             dt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
@@ -569,6 +609,8 @@ class FusedAdamEngine:
                 self._fault_c = c
                 for _ in range(warm):
                     self._raw_step()
+                if self._block_ok():
+                    self._run_steps(self.graph_steps)  # capture (and first replay) untimed
                 t = window(reps)
                 self._fault_c = None
                 restore()
@@ -615,13 +657,40 @@ class FusedAdamEngine:
             pend = self.pending
             self.pending = self.pipeline
             self._capture()
+            if self._block_ok():
+                self._capture(self.graph_steps)
             self.pending = pend
+        self._settle(est, restore)
         if multi:
             torch.cuda.synchronize()
             self.comm.barrier()
 
+    def _settle(self, step_s: float, restore) -> None:
+        """End the setup with ``MULTIGRAD_SETTLE_MS`` (60) of eager steps (no trajectory
+        rows; the optimizer state is restored afterwards), so the first real steps do not
+        start from an idle GPU.  Measured on one MI355X (profiles/narrow_sweep/README.md):
+        after the ~0.1 s of host work that follows the autotune windows, the forward kernel
+        ran 410 us for a few steps, then 500-585 us and only back at ~445 us after ~50 steps
+        -- the power controller's transient after an idle gap; a 20-step timing from there
+        measured ~1850 steps/s against ~2250 in steady state."""
+        ms = float(os.environ.get("MULTIGRAD_SETTLE_MS", "60"))
+        if ms <= 0 or self.device.type != "cuda":
+            return
+        n = int(min(2000, max(1, math.ceil(1e-3 * ms / max(step_s, 1e-5)))))
+        use_graph = self.use_graph
+        self._tuning = True
+        self.use_graph = False  # eager launches: the captured graphs write trajectory rows
+        try:
+            for _ in range(n):
+                self._raw_step()
+            restore()
+        finally:
+            self._tuning = False
+            self.use_graph = use_graph
+
 
     def _drain_all(self):
+        self._flush_exchange()
         for c in range(self.C):
             self._drain(c)
 
@@ -652,6 +721,26 @@ class FusedAdamEngine:
         self._ts_keep = None
         self.twoshot = None
         self.ready = False
+
+    def _ts_pack(self, c: int) -> bytes:
+        """Chunk c's two-shot exchange (reduce-scatter -> unbounded Adam -> all-gather) as
+        packed launch arguments for a compute launch that carries it (fused exchange)."""
+        a, b = self.own[c]
+        o, n = self.loc_off[c], self.loc_len[c]
+        tl = self._tl()
+        traj = None if tl is None else tl.reshape(-1)[o:]
+        return self.twoshot.pack(a, b - a, 1, m=self.m[o:o + n], v=self.v[o:o + n], traj=traj,
+                                 traj_stride=0 if traj is None else self.traj_loc.shape[1],
+                                 step=self.step_dev[c], host_step=self._hstep(), lr=self.lr,
+                                 b1=self.b1, b2=self.b2, eps=self.eps, max_blocks=self.ts_blocks)
+
+    def _flush_exchange(self):
+        """Launch the pending exchange of the last chunk on its own (fused exchange)."""
+        if self._x_pending is not None:
+            from ..ops._ext import ext
+            xs, self._x_pending = self._x_pending, None
+            if not self._inject_fault():
+                ext().xgmi_twoshot_launch_packed(xs)
 
     def _twoshot_update(self, c: int):
         """Chunk c: dense-gradient reduce-scatter + Adam on the owned slice + all-gather,
@@ -756,7 +845,9 @@ class FusedAdamEngine:
         self._ag[c] = None
 
     def drain(self):
-        """Join pending parameter all-gathers and apply a pending (pipelined) update."""
+        """Join pending parameter all-gathers and exchanges and apply a pending (pipelined)
+        update."""
+        self._flush_exchange()
         for c in range(self.C):
             self._drain(c)
         if self.pending:
@@ -823,6 +914,13 @@ class FusedAdamEngine:
                                                        args, **kw)
                 else:
                     kw = {} if epi is None else {"epilogue": epi}
+                    if i == 0 and self._x_pending is not None:
+                        # the previous step's exchange of the last chunk, in this launch's
+                        # first workgroups (this chunk's parameters are already complete)
+                        kw["exchange"] = self._x_pending
+                        self._x_pending = None
+                        if self._inject_fault():
+                            del kw["exchange"]
                     n = md.engine_forward_chunk(self.theta, self.slab[row * self.nS:], c, **kw)
                 folded = epi is not None
                 row += n
@@ -870,6 +968,14 @@ class FusedAdamEngine:
                            self.b1, self.b2, self.eps, self.bounds_loc, self.legacy,
                            traj_base=tb, traj_stride=(b - a) if tb is not None else 0,
                            host_step=self._hstep())
+        elif self.zero and self.twoshot is not None and not self.rccl_exchange and self.ts_fused:
+            # VJP_0, [VJP_1 + X_0], ..., [VJP_{C-1} + X_{C-2}]; X_{C-1} rides on the next
+            # step's first forward launch (or drain())
+            for c in range(self.C):
+                xs = self._ts_pack(c - 1) if c > 0 else None
+                with self._ph("vjp"):
+                    md.engine_vjp_into(self.theta, self.h, self.grad, chunk=c, exchange=xs)
+            self._x_pending = self._ts_pack(self.C - 1)
         elif self.zero and self.twoshot is not None and not self.rccl_exchange:
             for c in range(self.C):
                 with self._ph("vjp"):
@@ -953,7 +1059,10 @@ class FusedAdamEngine:
             return None
         return self.step_host if idx is None else idx
 
-    def _capture(self):
+    def _capture(self, k: int = 1):
+        """Capture ``k`` consecutive steps into one graph (k = 1: ``self.graph``; k > 1:
+        the block graph).  Every step inside reads and advances the device step counter,
+        so a block replays exactly like k one-step replays."""
         prep = getattr(self.model, "engine_prepare", None)
         if prep is not None:
             prep([self.rank] if self.owner else list(range(self.C)))
@@ -961,15 +1070,60 @@ class FusedAdamEngine:
         s.wait_stream(torch.cuda.current_stream())
         torch.cuda.current_stream().wait_stream(s)
         from .generic import _no_gc
-        self.graph = None
-        self.graph = torch.cuda.CUDAGraph()
+        g = torch.cuda.CUDAGraph()
+        pend = self.pending
         self._capturing = True
         try:
             with _no_gc():  # no CUDAGraph may be freed by the collector during a capture
-                with torch.cuda.graph(self.graph):
-                    self._enqueue_step()
+                with torch.cuda.graph(g):
+                    for _ in range(int(k)):
+                        self._enqueue_step()  # pipelined: sets pending for the next one
         finally:
             self._capturing = False
+            self.pending = pend
+        if k == 1:
+            self.graph = g
+        else:
+            self._kgraph = (int(k), g)
+
+    def _block_ok(self) -> bool:
+        """Whether steps may run as replays of a multi-step graph: graph mode, and no
+        per-step host work (the trajectory rows are written on the device)."""
+        return (self.use_graph and self.graph_steps > 1 and
+                (self.history.mode == "full" or self.traj_loc is not None))
+
+    def _run_steps(self, n: int):
+        """``n`` steps without the host-side history bookkeeping: blocks of
+        ``graph_steps`` steps replayed from one graph where allowed, the rest one by one."""
+        n = int(n)
+        K = self.graph_steps
+        while n > 0:
+            if n >= K and self._block_ok() and (self.pending or not self.pipeline):
+                if self._kgraph is None or self._kgraph[0] != K:
+                    self._capture(K)
+                self._kgraph[1].replay()
+                if self.pipeline:
+                    self.pending = True
+                self.step_host += K
+                n -= K
+            else:
+                self._raw_step()
+                n -= 1
+
+    def steps(self, n: int):
+        """Enqueue ``n`` optimizer steps (asynchronous on GPU): :meth:`step` ``n`` times,
+        with blocks of ``graph_steps`` steps replayed from one graph in graph mode."""
+        assert self.ready, "call setup() first"
+        n = int(n)
+        if n <= 0:
+            return
+        if not self._block_ok():
+            for _ in range(n):
+                self.step()
+            return
+        if self.step_host + n > self.nsteps and self.history.mode == "full":
+            raise RuntimeError("more steps than the trajectory buffer was sized for")
+        self._run_steps(n)
 
     def _raw_step(self):
         if self.use_graph and (self.pending or not self.pipeline):
@@ -1071,8 +1225,13 @@ class FusedAdamEngine:
             return ("RCCL reduce-scatter + all-gather (ZeRO-1), measured faster than the "
                     "two-shot kernel at setup")
         if self.zero and self.twoshot is not None:
-            sched = (f", {self.C} chunks on a side stream overlapping compute" if self.ts_side
-                     else f", {self.C} chunk(s) on the compute stream")
+            if self.ts_fused:
+                sched = (f", {self.C} chunks, each exchange in the first workgroups of the "
+                         f"next compute launch (fused exchange, one stream, no events)")
+            elif self.ts_side:
+                sched = f", {self.C} chunks on a side stream overlapping compute"
+            else:
+                sched = f", {self.C} chunk(s) on the compute stream"
             return ("xGMI two-shot kernel: reduce-scatter + Adam + all-gather in one launch per "
                     "chunk (self-tested)" + sched)
         if self.zero:
@@ -1218,16 +1377,22 @@ class FusedAdamEngine:
         from ..utils.hooks import StepHooks, driver_guard
         hooks = StepHooks(self.comm, callback)  # MULTIGRAD_CHECK_EVERY / MULTIGRAD_METRICS
         err_every = int(os.environ.get("MULTIGRAD_ERR_CHECK_EVERY", "100") or 0)
+        err_every = err_every if (self.oneshot is not None or self.twoshot is not None) else 0
+        ck_every = checkpoint_every if checkpoint_path else 0
         with driver_guard(self.comm):
             comm_bytes = self.comm_bytes_per_step()
-            for i in range(start, int(nsteps)):
-                self.step()
+            i, end = start, int(nsteps)
+            while i < end:
+                # steps up to the next host event run as one call (graph blocks)
+                n = 1 if hooks.active else min(
+                    [end - i] + [e - i % e for e in (err_every, ck_every) if e])
+                self.steps(n)
+                i += n
                 if hooks.active:
-                    hooks(i, self.loss, self, self.params, comm_bytes=comm_bytes)
-                if err_every and (self.oneshot is not None or self.twoshot is not None) and \
-                        (i + 1) % err_every == 0:
+                    hooks(i - 1, self.loss, self, self.params, comm_bytes=comm_bytes)
+                if err_every and i % err_every == 0:
                     self.check(collective=True)
-                if checkpoint_path and checkpoint_every and (i + 1) % checkpoint_every == 0:
+                if ck_every and i % ck_every == 0:
                     self.save_checkpoint(checkpoint_path)
             return self.trajectory()
 

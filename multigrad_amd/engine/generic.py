@@ -144,6 +144,8 @@ class GraphAdamEngine:
             graph = env.lower() not in ("0", "false", "off", "no")
         self.graph_req = graph
         self.graph = None
+        self._kgraph = None
+        self.graph_steps = max(1, int(os.environ.get("MULTIGRAD_GRAPH_STEPS", "16")))
         self.use_graph = False
         self.fallback_reason = None
         self.oneshot = None          # main-communicator one-shot (group loss)
@@ -294,6 +296,8 @@ class GraphAdamEngine:
         if self.mode == "eval":  # loss and summed gradient, packed for one host copy
             self.lg = torch.zeros(1 + P, **f32)
         self.graph = None
+        self._kgraph = None
+        self.graph_steps = max(1, int(os.environ.get("MULTIGRAD_GRAPH_STEPS", "16")))
         self.tuning = None
         self._times = {}
         self.fallback_reason = None
@@ -558,6 +562,60 @@ class GraphAdamEngine:
             self.graph.replay()
         cur.wait_stream(self._rs)
 
+    def _tuning_phase(self) -> bool:
+        return (self.graph_req is None and self.tuning is None and
+                self.nsteps > 3 * self._TUNE + self._TUNE_WARM)
+
+    def _block_ok(self) -> bool:
+        """Whether the next steps may replay a graph of ``graph_steps`` unrolled steps:
+        graph mode after its tuning, a step with no per-step key (the generators are seeded
+        once per replay), and no per-step host bookkeeping beyond the last parameters."""
+        return (self.use_graph and self.graph is not None and self.graph_steps > 1 and
+                self.key_mode is None and self.mode in ("adam", "sgd") and
+                not self._tuning_phase() and
+                (self.history.mode in ("full", "last") or self.traj_loc is not None))
+
+    def _capture_block(self, k: int):
+        """Capture ``k`` steps into one graph (after the one-step capture, which warmed up
+        the allocator and the kernels); each step reads and advances the device step."""
+        g = torch.cuda.CUDAGraph()
+        with _no_gc():
+            with torch.cuda.graph(g):
+                for _ in range(int(k)):
+                    self._body(None, None)
+        return g
+
+    def steps(self, n: int):
+        """``n`` optimizer steps: :meth:`step` one by one, or -- once graph mode is settled
+        for an unkeyed step -- replays of a graph of ``graph_steps`` unrolled steps (the
+        whole-loop capture of the reference's lax.scan, multigrad/mpi4jax/multigrad.py:
+        57-58, in blocks), with the remainder as one-step replays."""
+        n, K = int(n), self.graph_steps
+        while n > 0:
+            if n >= K and self._block_ok():
+                if self.step_host + K > self.nsteps:
+                    raise RuntimeError("more steps than the trajectory buffer was sized for")
+                if self._kgraph is None or self._kgraph[0] != K:
+                    self._kgraph = (K, self._capture_block(K))
+                self._kgraph[1].replay()
+                self.step_host += K
+                n -= K
+                if self.history.mode != "full" and self.traj_loc is None:
+                    self.history.record(self.step_host - 1, self.p[:self.P])
+            else:
+                self.step()
+                n -= 1
+
+    def _drive(self, nsteps: int, hooks, *hook_args, **hook_kw):
+        """Run ``nsteps`` steps; with per-step hooks one at a time, else as one
+        :meth:`steps` call (graph blocks)."""
+        if not hooks.active:
+            self.steps(nsteps)
+            return
+        for i in range(int(nsteps)):
+            self.step()
+            hooks(i, self.loss, *hook_args, **hook_kw)
+
     _TUNE = 6       # steps per timed window of the auto policy
     _TUNE_WARM = 3  # eager steps before the first window (lazy init, first launches, clocks)
 
@@ -718,10 +776,7 @@ class GraphAdamEngine:
         self.setup(guess, nsteps, learning_rate=learning_rate, history="last")
         hooks = StepHooks(self.comm, callback)
         with driver_guard(self.comm):
-            for i in range(int(nsteps)):
-                self.step()
-                if hooks.active:
-                    hooks(i, self.loss, None, self.params)
+            self._drive(nsteps, hooks, None, self.params)
         self.check("simple_grad_descent", collective=True)
         n = self.step_host
         res = GradDescentResult(loss=self.loss_hist[:n].clone(),
@@ -749,10 +804,7 @@ class GraphAdamEngine:
                 nS = sum(m[1] for m in getattr(self, "_S_meta", []) if m is not None)
                 return 0 if W == 1 else int(4 * (W - 1) * (nS + 2 * (self.P // W)))
 
-            for i in range(int(nsteps)):
-                self.step()
-                if hooks.active:
-                    hooks(i, self.loss, self, self.params, comm_bytes=comm_bytes)
+            self._drive(nsteps, hooks, self, self.params, comm_bytes=comm_bytes)
             traj = self.trajectory()
         self.close()
         return traj

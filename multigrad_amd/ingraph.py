@@ -17,6 +17,7 @@ all-reduced update.
 """
 from __future__ import annotations
 
+import os
 from typing import Callable
 
 import torch
@@ -59,13 +60,15 @@ def reduce_sum(partial_value: torch.Tensor, comm=None) -> torch.Tensor:
 
 
 def simple_grad_descent(data_dict, loss_and_grad_func: Callable, guess, learning_rate=0.01,
-                        nsteps=100, comm=None, graph=None):
+                        nsteps=100, comm=None, graph=None, block=None):
     """Fixed-step gradient descent with the whole loop device resident.
 
     ``loss_and_grad_func(data_dict, params) -> (loss, grad)`` returns this rank's partial
     loss and gradient (summed over ranks here, as in the reference).  Returns a pandas
     DataFrame with columns ``loss`` and ``params`` (one row per step, parameters at
-    which the loss was evaluated).
+    which the loss was evaluated).  ``block``: steps per captured graph (default
+    ``MULTIGRAD_GRAPH_STEPS``, 16); the run replays ``nsteps // block`` block graphs and one
+    graph of the remaining steps.
     """
     import pandas as pd
 
@@ -96,6 +99,11 @@ def simple_grad_descent(data_dict, loss_and_grad_func: Callable, guess, learning
     done = False
     if use_graph and n > 0:
         saved = params.clone()
+        # whole-loop capture in blocks: one graph of K unrolled steps replayed n // K times,
+        # plus one graph of the n % K remaining steps (the scan of the reference, without
+        # one graph node per optimizer step for long runs)
+        K = max(1, min(n, int(block) if block else int(os.environ.get("MULTIGRAD_GRAPH_STEPS", "16"))))
+        graphs = []
         try:
             s = torch.cuda.Stream()
             s.wait_stream(torch.cuda.current_stream())
@@ -104,9 +112,14 @@ def simple_grad_descent(data_dict, loss_and_grad_func: Callable, guess, learning
             torch.cuda.current_stream().wait_stream(s)
             params.copy_(saved)
             step.zero_()
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                body()
+            for k, reps in ((K, n // K), (n % K, 1)):
+                if k == 0 or reps == 0:
+                    continue
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    for _ in range(k):
+                        body()
+                graphs.append((g, reps))
             done = True
         except RuntimeError:
             # the user function is not capturable (host sync, dynamic shapes): run eagerly
@@ -118,8 +131,9 @@ def simple_grad_descent(data_dict, loss_and_grad_func: Callable, guess, learning
             params.copy_(saved)
             step.zero_()
         if done:
-            for _ in range(n):
-                g.replay()
+            for g, reps in graphs:
+                for _ in range(reps):
+                    g.replay()
     if not done:
         hooks = StepHooks(comm)  # MULTIGRAD_CHECK_EVERY / MULTIGRAD_METRICS (eager steps)
         with driver_guard(comm):

@@ -307,13 +307,18 @@ class PopulationSMFModel(OnePointModel):
         return self.shard.fwd_rows(max(h1 - h0, 1), self.bins.nb, True, self.bins.rel_tail,
                                    chunk, resid=True)
 
-    def engine_forward_chunk(self, theta, slab, chunk=None, epilogue=None) -> int:
+    def engine_forward_chunk(self, theta, slab, chunk=None, epilogue=None, exchange=None) -> int:
         # the engine always runs the VJP of a chunk after this forward at the same theta,
         # so the forward stores the VJP residuals (lanes layout) -- unless the VJP
         # recomputes (local slot order: few halos per population)
         return smf_forward_slab(theta, self.shard, self.bins, True, slab, chunk,
                                 resid=not self.shard.vjp_recompute, order=self._engine_order(),
-                                epilogue=self._epilogue_spec(epilogue))
+                                epilogue=self._epilogue_spec(epilogue), exchange=exchange)
+
+    def engine_fused_exchange_ok(self) -> bool:
+        """The forward / VJP launches can carry a packed two-shot exchange in their first
+        workgroups (``exchange=``): the tiles layout of the hashed placement."""
+        return self.shard.device.type == "cuda" and self.shard.layout == "tiles"
 
     def engine_forward_epilogue_ok(self) -> bool:
         """The sumstat epilogue can ride on the last forward launch sequence of a step
@@ -393,10 +398,10 @@ class PopulationSMFModel(OnePointModel):
                                oneshot.timeout_s, advance)
         return True
 
-    def engine_vjp_into(self, theta, h, grad, chunk=None):
+    def engine_vjp_into(self, theta, h, grad, chunk=None, exchange=None):
         return smf_vjp_into(theta, self.shard, self.bins, True, h, grad, chunk=chunk,
                             residuals_ready=True, order=self._engine_order(),
-                            recompute=self.shard.vjp_recompute)
+                            recompute=self.shard.vjp_recompute, exchange=exchange)
 
     def engine_vjp_adam_into(self, theta, h, m, v, unit_offset, step, host_step, lr, b1, b2,
                              eps, traj_base=None, traj_stride=0, chunk=None) -> bool:

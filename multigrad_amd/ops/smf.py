@@ -247,6 +247,18 @@ class PopulationShard:
         return not ((old is None and cls is None) or
                     (old is not None and cls is not None and torch.equal(old, cls)))
 
+    def per_edge_share(self) -> float:
+        """Share of the lane groups that hold a population of lane class != 0 (the narrow
+        populations of :meth:`set_lane_classes`): the groups the residual forward evaluates
+        by per-edge tails.  Cached per layout."""
+        if self.layout != "lanes" or self.lane_class is None or self.ngroups == 0:
+            return 0.0
+        if getattr(self, "_pe_share", None) is None:
+            sp = self.slot_pop.to("cpu", torch.int64)
+            c = torch.where(sp >= 0, self.lane_class[sp.clamp(min=0)], torch.zeros(1, dtype=torch.int64))
+            self._pe_share = float((c.reshape(-1, 64).amax(1) > 0).double().mean())
+        return self._pe_share
+
     def _order_key(self):
         key = self.order_counts
         if self.lane_class is None:
@@ -299,6 +311,7 @@ class PopulationShard:
             self.xi = None
         self.resid = None
         self.resid_epoch += 1
+        self._pe_share = None
 
     def fwd_schedule(self, chunk: Optional[int], nblocks: int):
         """Work distribution of the lanes forward over ``chunk`` with ``nblocks``
@@ -421,6 +434,14 @@ _GRID_CACHE: dict = {}
 LANES_FIX_BLOCKS = int(os.environ.get("MULTIGRAD_FIX_BLOCKS", "8"))
 
 
+# Share of per-edge lane groups (narrow populations, PopulationShard.per_edge_share) from
+# which the residual lanes forward runs the per-edge kernel for every group (LMODE 4)
+# instead of the Euler-Maclaurin kernel with its out-of-line per-edge call: measured on one
+# MI355X (profiles/narrow_sweep/) the EM kernel costs about 0.448 + 0.263 f ms per step at
+# a per-edge share f and the per-edge kernel 0.59 ms, so they cross near f = 0.5.
+PER_EDGE_SHARE = float(os.environ.get("MULTIGRAD_PER_EDGE_SHARE", "0.5"))
+
+
 def lanes_fix_blocks() -> int:
     """Slab rows of the fix-up launch of a residual lanes forward: LANES_FIX_BLOCKS when
     the extension runs the deferral list (MG_LANES_DEFER 1), else 0."""
@@ -494,15 +515,20 @@ def _user_theta(theta: torch.Tensor, shard: PopulationShard, order: str) -> torc
 def smf_forward_slab(theta: torch.Tensor, shard: PopulationShard, bins: SmfBins, log_sigma: bool,
                      slab: torch.Tensor, chunk: Optional[int] = None, resid: bool = False,
                      order: str = "user", update: Optional[dict] = None,
-                     epilogue: Optional[dict] = None) -> int:
+                     epilogue: Optional[dict] = None, exchange: Optional[bytes] = None) -> int:
     """Forward of the shard (or one population chunk) into per-workgroup slab rows;
     returns the number of rows written.  CPU: one row from the PyTorch reference.
     ``resid`` (lanes layout): also store the VJP residuals of these populations.
     ``order="internal"`` (lanes layout): ``theta`` is in the shard's internal parameter
     order (``shard.perm``), the order the fused engine keeps its vectors in; chunks are
-    the same population ranges in either order."""
+    the same population ranges in either order.  ``exchange``: a packed two-shot exchange
+    of another parameter chunk that the tiles forward runs in its first workgroups (fused
+    exchange); other paths launch it on its own first."""
     if order == "internal" and shard.layout != "lanes":
         raise ValueError("internal parameter order needs the lanes layout")
+    if exchange and (theta.device.type != "cuda" or shard.layout == "lanes"):
+        _launch_exchange(exchange)
+        exchange = None
     h0, h1 = shard.halo_range(chunk)
     if theta.device.type != "cuda":
         with torch.no_grad():
@@ -545,13 +571,14 @@ def smf_forward_slab(theta: torch.Tensor, shard: PopulationShard, bins: SmfBins,
                                        list(bins.scale), bool(log_sigma), g0, g1, slab, nblk,
                                        bins.rel_tail, rbuf, w_order, w_start, queues, upd, usc,
                                        shard.defer_buffer() if resid and lanes_fix_blocks() else None,
-                                       lanes_fix_blocks() if resid else 0, et, es, ep)
+                                       lanes_fix_blocks() if resid else 0, et, es, ep,
+                                       bool(resid and shard.per_edge_share() >= PER_EDGE_SHARE))
         if resid:
             shard.resid_epoch += 1
         return int(rows)
     assert epilogue is None, "the folded epilogue is a lanes-layout launch"
     ext().smf_forward(shard.x, shard.pop, theta, list(bins.edges), list(bins.scale),
-                      bool(log_sigma), h0, h1, slab, nblk, bins.rel_tail)
+                      bool(log_sigma), h0, h1, slab, nblk, bins.rel_tail, exchange or b"")
     return nblk
 
 
@@ -617,10 +644,17 @@ def smf_forward_into(theta: torch.Tensor, shard: PopulationShard, bins: SmfBins,
     return smf_slab_reduce(slab, nrows, bins, out)
 
 
+def _launch_exchange(exchange: Optional[bytes]) -> None:
+    """A packed two-shot exchange (parallel.xgmi.TwoShot.pack) launched on its own, for
+    the paths whose kernels do not carry one (enqueued before them: same stream order)."""
+    if exchange:
+        ext().xgmi_twoshot_launch_packed(exchange)
+
+
 def smf_vjp_into(theta: torch.Tensor, shard: PopulationShard, bins: SmfBins, log_sigma: bool,
                  h: torch.Tensor, grad: torch.Tensor, chunk: Optional[int] = None,
                  residuals_ready: bool = False, order: str = "user",
-                 recompute: bool = False) -> torch.Tensor:
+                 recompute: bool = False, exchange: Optional[bytes] = None) -> torch.Tensor:
     """Per-population VJP with edge weights ``h`` into ``grad`` (the chunk's parameters
     only).  CPU: autograd of the PyTorch reference restricted to the chunk's halos.
 
@@ -630,9 +664,14 @@ def smf_vjp_into(theta: torch.Tensor, shard: PopulationShard, bins: SmfBins, log
     does); otherwise the residual forward is recomputed here first.  ``order`` as in
     :func:`smf_forward_slab` (``grad`` is written in the same order as ``theta``).
     ``recompute`` (lanes layout): re-evaluate the halos instead of reading residuals
-    (``smf_vjp_lanes_rc_kernel``)."""
+    (``smf_vjp_lanes_rc_kernel``).  ``exchange``: a packed two-shot exchange of another
+    parameter chunk (fused exchange) that the tiles VJP runs in its first workgroups; other
+    paths launch it on its own first."""
     if order == "internal" and shard.layout != "lanes":
         raise ValueError("internal parameter order needs the lanes layout")
+    if exchange and (theta.device.type != "cuda" or shard.layout == "lanes"):
+        _launch_exchange(exchange)
+        exchange = None
     if theta.device.type != "cuda":
         h0, h1 = shard.halo_range(chunk)
         p0, p1 = (0, shard.npop) if chunk is None else (shard.chunk_pops[chunk], shard.chunk_pops[chunk + 1])
@@ -686,7 +725,8 @@ def smf_vjp_into(theta: torch.Tensor, shard: PopulationShard, bins: SmfBins, log
         t0, t1 = shard.chunk_tiles[chunk], shard.chunk_tiles[chunk + 1]
         g0, g1 = shard.chunk_giant[chunk], shard.chunk_giant[chunk + 1]
     E.smf_vjp(shard.x, shard.pop, theta, shard.tiles, t0, t1, h, list(bins.edges),
-              list(bins.scale), bool(log_sigma), grad, shard.partials, shard.giant[g0:g1])
+              list(bins.scale), bool(log_sigma), grad, shard.partials, shard.giant[g0:g1],
+              exchange or b"")
     return grad
 
 

@@ -342,6 +342,24 @@ class TwoShot:
                             float(b2), float(eps), self.timeout_s, float(traj_stride),
                             float(max_blocks)])
 
+    def pack(self, lo: int, n: int, mode: int, m=None, v=None, traj=None, traj_stride: int = 0,
+             step: Optional[torch.Tensor] = None, host_step: Optional[int] = None,
+             lr: float = 0.0, b1: float = 0.9, b2: float = 0.999, eps: float = 1e-8,
+             max_blocks: int = 0) -> bytes:
+        """The launch arguments of one Adam exchange (unbounded: ``mode`` 1), packed for a
+        compute launch that runs it in its first workgroups (fused exchange,
+        csrc/twoshot.h; ops.smf ``exchange=``).  Nothing is enqueued here."""
+        from ..ops._ext import ext
+        if not self.regions:
+            raise RuntimeError("two-shot context used after close() (its peer memory is "
+                               "unmapped)")
+        return ext().xgmi_twoshot_pack(
+            self.gpeers, self.tpeers, self.fpeers, self.rank, int(lo), int(n), self.numel,
+            int(mode), None, m, v, None, None, None, traj,
+            self._step0 if step is None else step, self.seq, self.err,
+            [float(-1 if host_step is None else host_step), float(lr), float(b1), float(b2),
+             float(eps), self.timeout_s, float(traj_stride), float(max_blocks)])
+
     def check(self, where: str = "", comm=None) -> None:
         OneShotAllReduce.check(self, where, comm)  # same err/seq protocol words
 

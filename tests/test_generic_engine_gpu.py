@@ -341,3 +341,43 @@ def test_graph_engine_randkey_with_host_syncs(graph):
     t = eng.run_adam(guess, nsteps=n, learning_rate=1e-3, randkey=7, callback=sync)
     assert eng.use_graph or graph is None
     torch.testing.assert_close(t, ref, rtol=0, atol=0)
+
+
+def test_graph_engine_block_replays_match_eager(monkeypatch):
+    """The generic engine's unkeyed graph mode replays blocks of MULTIGRAD_GRAPH_STEPS
+    steps after its one-step replays (Adam and gradient descent) with the eager results."""
+    from multigrad_amd.engine.generic import GraphAdamEngine
+    model, guess = _torch_pop()
+    ref = GraphAdamEngine(model, graph=False).run_adam(guess, nsteps=13, learning_rate=1e-3)
+    ref_gd = GraphAdamEngine(model, graph=False).run_simple_grad_descent(
+        guess, nsteps=13, learning_rate=1e-3)
+    monkeypatch.setenv("MULTIGRAD_GRAPH_STEPS", "5")
+    eng = GraphAdamEngine(model, graph=True)
+    t = eng.run_adam(guess, nsteps=13, learning_rate=1e-3)
+    assert eng.use_graph and eng.graph_steps == 5
+    torch.testing.assert_close(t, ref, rtol=1e-6, atol=1e-7)
+    gd = GraphAdamEngine(model, graph=True).run_simple_grad_descent(
+        guess, nsteps=13, learning_rate=1e-3)
+    torch.testing.assert_close(gd.params, ref_gd.params, rtol=1e-6, atol=1e-7)
+    torch.testing.assert_close(gd.loss, ref_gd.loss, rtol=1e-6, atol=1e-9)
+
+
+def test_ingraph_descent_block_capture_matches_eager():
+    """ingraph.simple_grad_descent with blocks of 4 steps and a remainder graph (11
+    steps) matches the eager loop."""
+    from multigrad_amd import ingraph
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(5000, generator=g).cuda()
+
+    def loss_and_grad(d, p):
+        r = d["x"][:, None] - p[None, :]
+        return 0.5 * (r * r).mean(), -r.mean(0)
+
+    guess = torch.tensor([0.5, -1.0], device="cuda")
+    a = ingraph.simple_grad_descent(dict(x=x), loss_and_grad, guess, 0.3, nsteps=11,
+                                    graph=True, block=4)
+    b = ingraph.simple_grad_descent(dict(x=x), loss_and_grad, guess, 0.3, nsteps=11, graph=False)
+    np.testing.assert_allclose(np.stack(a["params"].to_numpy()), np.stack(b["params"].to_numpy()),
+                               rtol=1e-6, atol=1e-7)
+    np.testing.assert_allclose(np.asarray(a["loss"], dtype=float), np.asarray(b["loss"], dtype=float),
+                               rtol=1e-6, atol=1e-9)

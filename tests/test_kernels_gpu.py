@@ -635,3 +635,71 @@ def test_headline_kernel_vs_fp64(monkeypatch):
     (gref,) = torch.autograd.grad(part, t64, dLdS)
     np.testing.assert_allclose(g0[:2 * npop_s].cpu(), gref.cpu(), rtol=2e-4,
                                atol=2e-5 * float(gref.abs().max()))
+
+
+@pytest.mark.parametrize("pipeline,owner", [("1", False), ("0", False), ("1", True)])
+def test_block_graph_replays_match_eager(monkeypatch, pipeline, owner):
+    """Whole-loop capture in blocks: graph mode replays graphs of
+    MULTIGRAD_GRAPH_STEPS unrolled steps (here 4, with a remainder of 3 single steps and a
+    pipelined first step) and gives the eager trajectory."""
+    from multigrad_amd.engine.fused import FusedAdamEngine
+    from multigrad_amd.models.population import PopulationSMFModel, make_population_data
+    monkeypatch.setenv("MULTIGRAD_PIPELINE", pipeline)
+    monkeypatch.setenv("MULTIGRAD_AUTOTUNE", "0")
+    data = make_population_data(num_params=6000, num_halos=300_000, seed=14, device=DEV)
+    model = PopulationSMFModel(aux_data=data)
+    model.set_target_from_truth()
+    ref = FusedAdamEngine(model, graph=False, owner=owner).run_adam(
+        data["guess"], nsteps=11, learning_rate=1e-3)
+    monkeypatch.setenv("MULTIGRAD_GRAPH_STEPS", "4")
+    eng = FusedAdamEngine(model, graph=True, owner=owner)
+    t = eng.run_adam(data["guess"], nsteps=11, learning_rate=1e-3)
+    assert eng.use_graph and eng.graph_steps == 4 and eng._kgraph is not None
+    torch.testing.assert_close(t, ref, rtol=1e-6, atol=1e-7)
+
+
+def test_per_edge_kernel_mode_matches_em_kernel(monkeypatch):
+    """LMODE 4 (the per-edge kernel for every group, chosen when most lane groups hold
+    narrow populations): sumstats against the fp64 oracle, and the pipelined engine's
+    trajectory against the Euler-Maclaurin kernel's with its out-of-line per-edge call."""
+    from multigrad_amd.engine.fused import FusedAdamEngine
+    from multigrad_amd.models.population import PopulationSMFModel, make_population_data
+    data = make_population_data(num_params=6000, num_halos=300_000, seed=17, device=DEV)
+    shard, bins = data["shard"], data["bins"]
+    model = PopulationSMFModel(aux_data=data)
+    model.set_target_from_truth()
+    guess = _narrow_guess(data, every=3)
+    runs = {}
+    for share in (2.0, 0.0):  # 2.0: never per-edge; 0.0: always
+        monkeypatch.setattr(S, "PER_EDGE_SHARE", share)
+        out = torch.zeros(bins.nbp, device=DEV)
+        S.smf_forward_into(guess, shard, bins, True, out, resid=True)
+        ref = S.smf_sumstats_reference(guess.double(), shard.x.double(), shard.pop, bins, True)
+        np.testing.assert_allclose(out[:bins.nb].cpu().double(), ref.cpu(), rtol=2e-5)
+        eng = FusedAdamEngine(model, graph=False)
+        runs[share] = eng.run_adam(guess, nsteps=5, learning_rate=1e-3)
+        assert eng.pipeline
+    # two evaluation methods (Euler-Maclaurin vs per-edge tails, ~1e-6 apart in the bin
+    # masses): Adam steps of lr 1e-3 on populations with near-zero gradients amplify that
+    # to ~1e-5 in a few parameters (measured 1.04e-5 after 5 steps); a wrong kernel would
+    # be off by whole steps
+    torch.testing.assert_close(runs[0.0], runs[2.0], rtol=1e-5, atol=1e-4)
+
+
+def test_narrow_populations_get_their_own_lane_groups():
+    """The fused engine groups narrow populations (bin width > 0.5 sigma at the guess) into
+    lane groups of their own: with 1% of populations narrow, about 1% of the groups take
+    the per-edge path (without the layout hint, ~half of them would)."""
+    from multigrad_amd.engine.fused import FusedAdamEngine
+    from multigrad_amd.models.population import PopulationSMFModel, make_population_data
+    data = make_population_data(num_params=200_000, num_halos=2_700_000, seed=4, device=DEV,
+                                narrow_frac=0.01)
+    model = PopulationSMFModel(aux_data=data)
+    model.set_target_from_truth()
+    before = model.lane_fallback_groups(data["guess"])
+    eng = FusedAdamEngine(model, graph=False)
+    eng.setup(data["guess"], 3, learning_rate=1e-3)
+    after = model.lane_fallback_groups(data["guess"])
+    assert before[0] > 0.3 * before[1] and after[0] < 0.05 * after[1], (before, after)
+    eng.steps(3)
+    assert np.isfinite(eng.last_loss())

@@ -423,3 +423,28 @@ def test_autotune_falls_back_to_rccl_when_no_peer_schedule_survives():
     assert tun["chosen"]["rccl_exchange"], tun
     assert "RCCL" in rec["config"]["grad_collective"]
     assert np.isfinite(rec["loss_last"])
+
+
+def _engine_hashed_fused(rank, size, fused, chunks):
+    os.environ["MULTIGRAD_TWOSHOT_FUSED"] = "on" if fused else "off"
+    os.environ["MULTIGRAD_TWOSHOT_SIDE_STREAM"] = "off"
+    return _engine_hashed(rank, size, True, False, chunks, "auto", None, "off")
+
+
+@pytest.mark.parametrize("size,chunks", [(2, 2), (2, 3), (4, 2), (8, 4)])
+def test_engine_hashed_fused_exchange_matches_serial(size, chunks):
+    """the fused exchange -- chunk c-1's two-shot exchange in the first
+    workgroups of chunk c's VJP launch, the last chunk's in the next step's first forward
+    launch (no side stream, no events) -- gives the same bits as the serial two-shot
+    schedule (2, 4 and 8 processes on one GPU), and with 2 ranks as the RCCL/gloo path."""
+    ser = run_distributed(_engine_hashed_fused, size, False, chunks, timeout=900)
+    fus = run_distributed(_engine_hashed_fused, size, True, chunks, timeout=900)
+    assert all(r[1] and r[5] == chunks and "fused exchange" in r[4] for r in fus), fus[0][4]
+    assert not any("fused exchange" in r[4] for r in ser)
+    for r in range(size):
+        np.testing.assert_array_equal(fus[r][0], fus[0][0])
+        np.testing.assert_array_equal(fus[r][0], ser[r][0])
+    if size == 2:
+        ref = run_distributed(_engine_hashed, 2, False, False, chunks, "auto", None, "off",
+                              timeout=600)
+        np.testing.assert_array_equal(fus[0][0], ref[0][0])

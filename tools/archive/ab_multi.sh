@@ -1,7 +1,7 @@
 #!/bin/bash
 # A/B several variants/<name>/_C.so builds against the in-tree one on the same box, REPS
 # rounds of (base, v1, v2, ...), printing each run's last output line:
-#   REPS=2 bash tools/ab_multi.sh "v1 v2" <script.py> [args...]
+#   REPS=2 bash tools/archive/ab_multi.sh "v1 v2" <script.py> [args...]
 set -u
 names=$1; shift
 cp multigrad_amd/_C.so /tmp/_C_base.so

@@ -1,7 +1,7 @@
 #!/bin/bash
 # A/B any timing script between the in-tree _C.so and variants/<name>/_C.so on the same box,
 # alternating runs, printing each run's last output line:
-#   bash tools/ab_script_so.sh <name> <script.py> [args...]
+#   bash tools/archive/ab_script_so.sh <name> <script.py> [args...]
 set -u
 name=$1; shift
 cp multigrad_amd/_C.so /tmp/_C_base.so

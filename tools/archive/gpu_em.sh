@@ -10,7 +10,7 @@ cd "$R"
 timeout -k 10 400 python -u -m pytest tests/test_kernels_gpu.py -x -v --timeout 120 \
   --timeout-method thread > "$O/pytest_kernels.log" 2>&1
 rc=$?; tail -5 "$O/pytest_kernels.log"; [ $rc -eq 0 ] || exit $rc
-bash tools/ab_script_so.sh em0 bench.py --steps 50 --warmup 5 --no-count-launches > "$O/ab.log" 2>&1
+bash tools/archive/ab_script_so.sh em0 bench.py --steps 50 --warmup 5 --no-count-launches > "$O/ab.log" 2>&1
 rc=$?; cut -c1-260 "$O/ab.log"; [ $rc -eq 0 ] || exit $rc
 export TMPDIR=/tmp
 cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof" -o bench \

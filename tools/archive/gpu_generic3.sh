@@ -19,6 +19,6 @@ for i in 1 2; do
   grep '^{' "$O/bench$i.log" | cut -c1-200
 done
 if [ -f variants/emonly/_C.so ]; then
-  bash tools/ab_script_so.sh emonly bench.py --steps 50 --warmup 5 --no-count-launches > "$O/ab_emonly.log" 2>&1
+  bash tools/archive/ab_script_so.sh emonly bench.py --steps 50 --warmup 5 --no-count-launches > "$O/ab_emonly.log" 2>&1
   cut -c1-160 "$O/ab_emonly.log"
 fi

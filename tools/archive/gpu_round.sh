@@ -1,6 +1,6 @@
 #!/bin/bash
 # One GPU session: tests, smoke, short bench. Stops at the first crash/timeout.
-# Usage: bash tools/gpu_round.sh [bench args...]
+# Usage: bash tools/archive/gpu_round.sh [bench args...]
 set -u
 mkdir -p gpurun_out
 ok_or_fail() {  # continue on pass (0) or ordinary test failure (1); stop on anything else

@@ -9,4 +9,4 @@ timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_ou
 tail -1 gpurun_out/smoke.log
 timeout -k 10 300 python bench.py > gpurun_out/bench.log 2>&1
 grep '^{' gpurun_out/bench.log
-bash tools/bench_2rank_gloo.sh
+bash tools/archive/bench_2rank_gloo.sh

@@ -11,7 +11,7 @@ timeout -k 10 400 python -u -m pytest tests/test_kernels_gpu.py -x -v --timeout 
   --timeout-method thread > "$O/pytest_kernels.log" 2>&1
 rc=$?; tail -3 "$O/pytest_kernels.log"; [ $rc -eq 0 ] || exit $rc
 for v in "$@"; do
-  bash tools/ab_script_so.sh $v tools/uncached_theta_bench.py > "$O/ab_$v.log" 2>&1
+  bash tools/archive/ab_script_so.sh $v tools/uncached_theta_bench.py > "$O/ab_$v.log" 2>&1
   rc=$?; cut -c1-330 "$O/ab_$v.log"; [ $rc -eq 0 ] || exit $rc
 done
 bash tools/pmc_kernels.sh --layout tiles --halos 16777216

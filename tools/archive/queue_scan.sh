@@ -1,6 +1,6 @@
 #!/bin/bash
 # Headline bench over the number of dynamic forward work queues (MULTIGRAD_FWD_QUEUES),
-# alternating values, two rounds: bash tools/queue_scan.sh [bench args...]
+# alternating values, two rounds: bash tools/archive/queue_scan.sh [bench args...]
 set -u
 for rep in 1 2; do
   for q in 64 128 256 512 1024; do
