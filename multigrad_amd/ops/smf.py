@@ -437,9 +437,10 @@ LANES_FIX_BLOCKS = int(os.environ.get("MULTIGRAD_FIX_BLOCKS", "8"))
 # Share of per-edge lane groups (narrow populations, PopulationShard.per_edge_share) from
 # which the residual lanes forward runs the per-edge kernel for every group (LMODE 4)
 # instead of the Euler-Maclaurin kernel with its out-of-line per-edge call: measured on one
-# MI355X (profiles/narrow_sweep/) the EM kernel costs about 0.448 + 0.263 f ms per step at
-# a per-edge share f and the per-edge kernel 0.59 ms, so they cross near f = 0.5.
-PER_EDGE_SHARE = float(os.environ.get("MULTIGRAD_PER_EDGE_SHARE", "0.5"))
+# MI355X (profiles/narrow_sweep/, rocprof kernel averages) the EM kernel takes about
+# 446 + 410 f us at a per-edge share f and the per-edge kernel 617-627 us, so they cross
+# near f = 0.42.
+PER_EDGE_SHARE = float(os.environ.get("MULTIGRAD_PER_EDGE_SHARE", "0.45"))
 
 
 def lanes_fix_blocks() -> int:
