@@ -33,7 +33,8 @@ def fused_row(params, halos, steps, warm, K, mode):
         model.set_target_from_truth()
         _CACHE[key] = (data, model)
     data, model = _CACHE[key]
-    eng = FusedAdamEngine(model, graph=mode != "eager")
+    eng = FusedAdamEngine(model, graph=not mode.startswith("eager"))
+    eng.device_step = mode == "eager-dev"
     eng.graph_steps = K if mode == "graph-K" else 1
     eng.setup(data["guess"], warm + steps + 1, learning_rate=1e-3)
     eng.steps(warm)
@@ -44,7 +45,7 @@ def fused_row(params, halos, steps, warm, K, mode):
     eng.drain()
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / steps
-    assert eng.use_graph == (mode != "eager")
+    assert eng.use_graph == (not mode.startswith("eager"))
     eng.close()
     return dt
 
@@ -59,7 +60,7 @@ def generic_row(params, halos, steps, warm, K, mode):
         PopulationSMFModel(aux_data=data).set_target_from_truth()
         _CACHE[key] = (TorchPopulationSMFModel(aux_data=torch_population_data(data)), data["guess"])
     m, guess = _CACHE[key]
-    eng = GraphAdamEngine(m, graph=mode != "eager")
+    eng = GraphAdamEngine(m, graph=not mode.startswith("eager"))
     eng.graph_steps = K if mode == "graph-K" else 1
     eng.setup(guess, warm + steps, learning_rate=1e-3)
     eng.steps(warm)
@@ -82,7 +83,7 @@ def ingraph_row(params, halos, steps, warm, K, mode):
         return 0.5 * (r * r).mean(), -r.mean(0)
 
     guess = torch.zeros(params, device="cuda")
-    kw = dict(graph=mode != "eager", block=K if mode == "graph-K" else 1)
+    kw = dict(graph=not mode.startswith("eager"), block=K if mode == "graph-K" else 1)
     ingraph.simple_grad_descent(dict(x=x), loss_and_grad, guess, 0.1, nsteps=warm, **kw)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -100,6 +101,9 @@ def main(argv=None):
     ap.add_argument("--warm", type=int, default=40)
     ap.add_argument("--K", type=int, default=16)
     ap.add_argument("--repeats", type=int, default=3)
+    ap.add_argument("--modes", default="eager,graph-1,graph-K",
+                    help="eager, eager-dev (fused rows: eager launches on the device step "
+                         "counter), graph-1, graph-K")
     ap.add_argument("--rows", default="fused,owner_proxy,generic_small,generic_large,ingraph")
     a = ap.parse_args(argv)
     rows = {
@@ -109,7 +113,7 @@ def main(argv=None):
         "generic_large": (generic_row, 200_000, 4_000_000),
         "ingraph": (ingraph_row, 3, 20_000),
     }
-    modes = ("eager", "graph-1", "graph-K")
+    modes = tuple(a.modes.split(","))
     res = {}
     for name in a.rows.split(","):
         fn, params, halos = rows[name]
@@ -120,12 +124,11 @@ def main(argv=None):
         res[name] = {m: round(statistics.median(v), 4) for m, v in times.items()}
         res[name]["all_ms"] = {m: [round(t, 4) for t in v] for m, v in times.items()}
         print(json.dumps({name: res[name]}), flush=True)
-    print("| row | eager ms/step | 1-step replay | %d-step replay | K-step / eager |" % a.K)
-    print("|---|---|---|---|---|")
+    print("| row | " + " | ".join(f"{m} ms/step" for m in modes) + " | K-step / eager |")
+    print("|---" * (len(modes) + 2) + "|")
     for name, r in res.items():
-        print(f"| {name} | {r['eager']:.4f} | {r['graph-1']:.4f} | {r['graph-K']:.4f} | "
-              f"{r['eager'] / r['graph-K']:.3f}x |")
-
+        ratio = (f"{r['eager'] / r['graph-K']:.3f}x" if "eager" in r and "graph-K" in r else "-")
+        print(f"| {name} | " + " | ".join(f"{r[m]:.4f}" for m in modes) + f" | {ratio} |")
 
 if __name__ == "__main__":
     main()

@@ -183,6 +183,10 @@ class FusedAdamEngine:
         self._kgraph = None
         self.graph = None
         self._capturing = False
+        # eager launches of a pipelined step that read/advance the device step counter like
+        # graph replays do (benchmarks/graph_modes.py "eager-dev": separates the cost of the
+        # device counter from the cost of graph dispatch); MULTIGRAD_DEVICE_STEP=1
+        self.device_step = _env_flag("MULTIGRAD_DEVICE_STEP", False)
         self.pending = False
         self.pipeline = False
         self.ready = False
@@ -1055,7 +1059,7 @@ class FusedAdamEngine:
         """The 0-based step for eager launches; None inside a graph capture and for every
         launch of a graph-mode engine (the Adam kernels then keep the step in device
         memory, so graph replays and eager launches agree)."""
-        if self._capturing or (self.use_graph and self.pipeline):
+        if self._capturing or ((self.use_graph or self.device_step) and self.pipeline):
             return None
         return self.step_host if idx is None else idx
 

@@ -7,7 +7,7 @@ export TMPDIR=/tmp
 row=${1:-fused}
 out=gpurun_out/gbt
 mkdir -p $out
-for mode in eager graph-1 graph-K; do
+for mode in eager eager-dev graph-1 graph-K; do
   timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $out/$mode -o k -- \
     python3 -c "
 import sys; sys.path.insert(0, '.')
@@ -31,6 +31,14 @@ for r in k:
     prev = e
 print(sys.argv[2], {n: round(statistics.median(v), 1) for n, v in dur.items()},
       "gap median %.2f us, max %.2f us, sum %.1f us over %d kernels" % (statistics.median(gaps), max(gaps), sum(gaps), len(k)))
+# gap before each kernel, by (previous kernel -> kernel): where the idle time sits
+pair = {}
+for a, b, g in zip(k, k[1:], gaps):
+    na = a['Kernel_Name'].split('(')[0].split('<')[0][-24:]
+    nb = b['Kernel_Name'].split('(')[0].split('<')[0][-24:]
+    pair.setdefault(na + ' -> ' + nb, []).append(g)
+for n, v in sorted(pair.items()):
+    print("   %-52s n=%2d median %6.2f us  max %6.2f us" % (n, len(v), statistics.median(v), max(v)))
 PY
   find $out/$mode -type f -delete
 done
