@@ -61,6 +61,7 @@ from typing import Optional
 
 import torch
 
+from ._stream import EngineStream, make_engine_stream, on_engine_stream
 from ..ops.adam import adam_step_
 from ..optim.adam import History
 from ..optim.transforms import Bounds
@@ -158,6 +159,30 @@ class GraphAdamEngine:
         self._cap_key = _CaptureKey(self)
         self.key_mode = None     # None | "step" | "const"
         self.ready = False
+        self._es = None          # the engine's own stream (stream())
+        self._dev_step_stale = False  # eager steps ran since the device step was last set
+
+    # ------------------------------------------------------------------ stream
+    def _engine_stream(self):
+        dev = getattr(self, "device", None)
+        self._es = make_engine_stream(self._es, dev if dev is not None
+                                      else self.members[0].param_device())
+        return self._es
+
+    def stream(self):
+        """Context manager: the current stream becomes the engine's own (non-default) HIP
+        stream, ordered after the caller's stream on entry and before it on exit.
+
+        Every public method of the engine runs its GPU work -- eager steps, captures, graph
+        replays, and the user hooks and callbacks it calls -- inside this context.  On this
+        ROCm runtime a graph replay that follows a host synchronisation and any launch on
+        the legacy default stream since the graph's previous replay computes wrong results
+        (garbage in the graph's intermediates), while the same schedules with nothing
+        launched on the default stream match eager launches bit for bit
+        (tools/dbg/torch_replay_bisect.py, torch only; docs/design.md "Graph replays and the
+        default stream").  User code that calls :meth:`step` directly and launches its own
+        GPU work between the calls should do that work inside ``with engine.stream():``."""
+        return EngineStream(self)
 
     # ------------------------------------------------------------------ keys
     def _next_generator(self, device) -> torch.Generator:
@@ -192,6 +217,7 @@ class GraphAdamEngine:
                 g.manual_seed(key.seed)
 
     # ------------------------------------------------------------------ setup
+    @on_engine_stream
     def setup(self, guess, nsteps: int, param_bounds=None, learning_rate: float = 0.01,
               b1: float = 0.9, b2: float = 0.999, eps: float = 1e-8, history="full",
               legacy_bounds_jacobian: bool = False, randkey=None, const_randkey: bool = False):
@@ -278,6 +304,7 @@ class GraphAdamEngine:
             self.bounds_loc = bounds
             self.u = bounds.forward(self.p).contiguous() if bounds is not None else self.p
         self.step_dev = torch.zeros(2, dtype=torch.int32, device=dev)
+        self._dev_step_stale = False
         self.loss = torch.zeros(1, **f32)
         self.nsteps = int(nsteps)
         self.step_host = 0
@@ -327,6 +354,7 @@ class GraphAdamEngine:
         self.ready = True
         return self
 
+    @on_engine_stream
     def close(self) -> None:
         """Give the two-shot context back to the communicator's pool (collective: every
         rank closes its engine the same way); setup() calls it before re-connecting."""
@@ -543,24 +571,17 @@ class GraphAdamEngine:
         return graph
 
     def _replay(self, key) -> None:
-        """Replay the captured step.  A step with graph-registered generators is replayed
-        on the engine's own stream, ordered after the current stream by an event and back:
-        launched on the default stream right after a host synchronisation, such a graph
-        computed wrong sums downstream of its RNG op on this ROCm runtime (the RNG output
-        itself was right), reproducibly, while the side-stream launch matched the eager
-        step bit for bit with and without synchronisation (tools/dbg/auto_keys10.py,
-        docs/design.md)."""
+        """Replay the captured step (on the engine stream, like every launch of the engine:
+        see :meth:`stream`).  After eager steps, the device step counter is set from the
+        host first (eager steps keep the count on the host)."""
+        self._sync_dev_step()
         self._seed_generators(key)
-        if not self._gens:
-            self.graph.replay()
-            return
-        cur = torch.cuda.current_stream()
-        if getattr(self, "_rs", None) is None:
-            self._rs = torch.cuda.Stream()
-        self._rs.wait_stream(cur)
-        with torch.cuda.stream(self._rs):
-            self.graph.replay()
-        cur.wait_stream(self._rs)
+        self.graph.replay()
+
+    def _sync_dev_step(self) -> None:
+        if self._dev_step_stale:
+            self.step_dev[0] = self.step_host
+            self._dev_step_stale = False
 
     def _tuning_phase(self) -> bool:
         return (self.graph_req is None and self.tuning is None and
@@ -585,6 +606,7 @@ class GraphAdamEngine:
                     self._body(None, None)
         return g
 
+    @on_engine_stream
     def steps(self, n: int):
         """``n`` optimizer steps: :meth:`step` one by one, or -- once graph mode is settled
         for an unkeyed step -- replays of a graph of ``graph_steps`` unrolled steps (the
@@ -597,6 +619,7 @@ class GraphAdamEngine:
                     raise RuntimeError("more steps than the trajectory buffer was sized for")
                 if self._kgraph is None or self._kgraph[0] != K:
                     self._kgraph = (K, self._capture_block(K))
+                self._sync_dev_step()
                 self._kgraph[1].replay()
                 self.step_host += K
                 n -= K
@@ -624,17 +647,16 @@ class GraphAdamEngine:
         ``_TUNE`` eager steps, then the capture and one untimed replay, then a window of
         ``_TUNE`` replays; each window is timed as a whole (no synchronisation inside it,
         so eager launches overlap the GPU as in steady state).  Replay is kept only if it
-        beats eager by 3% -- a collective decision -- and then simply continues, so a
-        replay never follows eager steps of the tuning (such a default-stream replay after
-        eager work and a host synchronisation computed wrong sums on this runtime, see
-        _replay).  Measured on one MI355X (profiles/generic_engine.md): replay wins only
-        when the step is launch bound and loses when it is GPU bound."""
+        beats eager by 3% -- a collective decision -- and then simply continues.  Measured
+        on one MI355X (profiles/graph_modes/): replay wins when the step is launch bound
+        and loses slightly when it is GPU bound."""
         import time
         k, T, W = self.step_host, self._TUNE, self._TUNE_WARM
         # phase: -1 warm-up, 0 eager window, 1 first (untimed) replay, 2 replay window
         ph = -1 if k < W else 0 if k < W + T else 1 if k == W + T else 2
         if ph >= 1 and self.graph is None:
             self.step_dev[0] = k   # eager steps keep the count on the host
+            self._dev_step_stale = False
             try:
                 self.graph = self._capture()
             except Exception as exc:  # noqa: BLE001
@@ -644,6 +666,7 @@ class GraphAdamEngine:
                 self.use_graph = False
                 self.fallback_reason = f"capture failed: {type(exc).__name__}: {exc}"
                 self._body(k, key)
+                self._dev_step_stale = True
                 return
         if k in (W, W + T + 1):
             torch.cuda.synchronize()
@@ -652,6 +675,7 @@ class GraphAdamEngine:
             self._replay(key)
         else:
             self._body(k, key)
+            self._dev_step_stale = True
         if k in (W + T - 1, W + 2 * T):
             torch.cuda.synchronize()
             self._times[ph] = time.perf_counter() - self._t0
@@ -666,6 +690,7 @@ class GraphAdamEngine:
                 self.graph = None
                 self.fallback_reason = f"eager measured faster ({te * 1e3:.3f} vs {tg * 1e3:.3f} ms/step)"
 
+    @on_engine_stream
     def step(self):
         assert self.ready, "call setup() first"
         if self.step_host >= self.nsteps and (self.history.mode == "full" or self.traj_loc is not None
@@ -692,6 +717,7 @@ class GraphAdamEngine:
             self._replay(key)
         else:
             self._body(self.step_host, key)
+            self._dev_step_stale = True
         self.step_host += 1
         if self.history.mode != "full" and self.traj_loc is None:
             self.history.record(self.step_host - 1, self.p[:self.P])
@@ -707,15 +733,18 @@ class GraphAdamEngine:
                 ctx.check(where or f"generic engine step {self.step_host}",
                           comm=md.comm if collective else None)
 
+    @on_engine_stream
     def last_loss(self) -> float:
         v = float(self.loss.item())
         self.check("last_loss")
         return v
 
+    @on_engine_stream
     def params(self) -> torch.Tensor:
         self.check("params", collective=True)
         return self.p[:self.P].reshape(self.shape).clone()
 
+    @on_engine_stream
     def trajectory(self) -> torch.Tensor:
         self.check("trajectory", collective=True)
         if self.traj_loc is not None:
@@ -729,6 +758,7 @@ class GraphAdamEngine:
         t = self.history.result()[:, :self.P] if self.history.mode == "full" else self.history.result()
         return t.reshape((t.shape[0],) + self.shape)
 
+    @on_engine_stream
     def evaluator(self, x0, randkey=None):
         """``f(x) -> (loss, grad)`` replaying one captured evaluation of the distributed
         chain rule (autograd forward, sumstat all-reduce, cotangent, VJP, gradient sum):
@@ -754,17 +784,19 @@ class GraphAdamEngine:
             kw.pop("randkey", None)  # the engine holds the (constant) key
             if kw:
                 raise TypeError(f"the captured evaluator takes no keywords: {sorted(kw)}")
-            self.p[:P].copy_(torch.as_tensor(x).reshape(-1))
-            key = self._step_key()
-            if self.use_graph:
-                self._replay(key)
-            else:
-                self._body(None, key)
-            out = self.lg.cpu()  # loss and gradient in ONE device->host copy
+            with self.stream():
+                self.p[:P].copy_(torch.as_tensor(x).reshape(-1))
+                key = self._step_key()
+                if self.use_graph:
+                    self._replay(key)
+                else:
+                    self._body(None, key)
+                out = self.lg.cpu()  # loss and gradient in ONE device->host copy
             return out[0], out[1:].reshape(shape)
 
         return f
 
+    @on_engine_stream
     def run_simple_grad_descent(self, guess, nsteps: int = 100, learning_rate: float = 0.01,
                                 callback=None):
         """Fixed-rate gradient descent with the reference's result contract
@@ -785,6 +817,7 @@ class GraphAdamEngine:
         self.close()
         return res
 
+    @on_engine_stream
     def run_adam(self, guess, nsteps: int = 100, param_bounds=None, learning_rate: float = 0.01,
                  b1: float = 0.9, b2: float = 0.999, eps: float = 1e-8, history="full",
                  legacy_bounds_jacobian: bool = False, callback=None, randkey=None,

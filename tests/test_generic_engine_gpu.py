@@ -381,3 +381,28 @@ def test_ingraph_descent_block_capture_matches_eager():
                                rtol=1e-6, atol=1e-7)
     np.testing.assert_allclose(np.asarray(a["loss"], dtype=float), np.asarray(b["loss"], dtype=float),
                                rtol=1e-6, atol=1e-9)
+
+
+@pytest.mark.parametrize("keyed", [False, True])
+def test_graph_engine_replays_after_eager_steps_with_syncs(keyed):
+    """Replays that follow eager steps, with a host synchronisation and a user kernel
+    (inside engine.stream()) after every step -- the schedules that computed wrong results
+    when the engine launched on the default stream (a HIP runtime defect reproduced with
+    torch alone, tools/dbg/torch_replay_bisect.py).  Every launch of the engine now runs on
+    its own stream, so the order eager / replay / eager / replay gives the eager trajectory."""
+    from multigrad_amd.engine.generic import GraphAdamEngine
+    m, guess = _stoch_pop() if keyed else _torch_pop()
+    kw = dict(randkey=9) if keyed else {}
+    sched = "eeeggggeeeggg"
+    ref = m.run_adam(guess, nsteps=len(sched), learning_rate=1e-3, use_engine=False, **kw)
+    eng = GraphAdamEngine(m, graph=True)
+    eng.setup(guess, nsteps=len(sched), learning_rate=1e-3, **kw)
+    scratch = torch.zeros(1, device=DEV)
+    for mode in sched:
+        eng.use_graph = mode == "g"
+        eng.step()
+        with eng.stream():
+            scratch.add_(1)
+        torch.cuda.synchronize()
+    assert eng.graph is not None
+    torch.testing.assert_close(eng.trajectory(), ref, rtol=1e-6, atol=1e-7)

@@ -1,7 +1,14 @@
-"""Generic engine: graph replays that FOLLOW eager steps (e.g. an auto-policy order eager /
-replay / eager / replay).  Prints, per schedule and replay stream, the largest trajectory
-deviation from the eager reference, with and without a host synchronisation after each
-step.  Usage (one GPU): python tools/dbg/eager_then_replay.py"""
+"""Generic engine: graph replays that FOLLOW eager steps (an order eager / replay / eager /
+replay), through the engine's public API (``use_graph`` switched between ``step()`` calls).
+Prints, per schedule, the largest trajectory deviation from the eager reference, with and
+without a host synchronisation after each step, and with a user kernel between the steps
+issued inside ``engine.stream()``.  Every line should read 0.0e+00.
+
+The last section shows the one schedule the engine cannot protect: user work launched on
+the legacy DEFAULT stream between direct ``step()`` calls, with host synchronisations
+(the HIP runtime defect of tools/dbg/torch_replay_bisect.py, case user_null; see
+docs/design.md "Graph replays and the default stream").
+Usage (one GPU): python tools/dbg/eager_then_replay.py"""
 import os
 import sys
 
@@ -20,40 +27,35 @@ g = data["guess"]
 m = TorchPopulationSMFModel(aux_data=torch_population_data(data))
 N = 20
 ref = m.run_adam(g, nsteps=N, learning_rate=1e-3, use_engine=False)
+scratch = torch.zeros(1, device=dev)
 
 
-def run(schedule, side, sync):
+def run(schedule, sync, user=None):
     eng = GraphAdamEngine(m, graph=True)
     eng.setup(g, nsteps=N, learning_rate=1e-3)
-    prev = None
-    for k, mode in enumerate(schedule):
-        if mode == "g":
-            if eng.graph is None or prev == "e":
-                eng.step_dev[0] = k
-            if eng.graph is None:
-                eng.graph = eng._capture()
-            if side:
-                s = torch.cuda.Stream()
-                s.wait_stream(torch.cuda.current_stream())
-                with torch.cuda.stream(s):
-                    eng.graph.replay()
-                torch.cuda.current_stream().wait_stream(s)
-            else:
-                eng.graph.replay()
-        else:
-            eng._body(k, None)
-        eng.step_host += 1
+    for mode in schedule:
+        eng.use_graph = mode == "g"
+        eng.step()
+        if user == "engine_stream":
+            with eng.stream():
+                scratch.add_(1)
+        elif user == "default_stream":
+            scratch.add_(1)
         if sync:
             torch.cuda.synchronize()
-        prev = mode
     t = eng.trajectory()
+    torch.cuda.synchronize()
     d = (t - ref).abs().amax(dim=1)
-    bad = [i for i in range(d.numel()) if float(d[i]) > 1e-5]
+    bad = [i for i in range(d.numel()) if not float(d[i]) <= 1e-5]
     return "%.1e first_bad_row=%s" % (float(d.max()), bad[0] if bad else None)
 
 
-for sched in ("eeeeeggggggggggggggg", "eeeeeggggggeeeeegggg", "eeeeeggggggeeeeeeeee"):
-    for side in (False, True):
-        for sync in (False, True):
-            print(sched, "side" if side else "default", "sync" if sync else "nosync",
-                  run(sched, side, sync), flush=True)
+for sched in ("eeeeeggggggggggggggg", "eeeeeggggggeeeeegggg", "eeeeeggggggeeeeeeeee",
+              "gggggggggggggggggggg"):
+    for sync in (False, True):
+        for user in (None, "engine_stream"):
+            print(sched, "sync" if sync else "nosync", user or "-", run(sched, sync, user),
+                  flush=True)
+print("-- not protected (user kernels on the default stream between direct step() calls):")
+for sched in ("eeeeeggggggeeeeegggg", "gggggggggggggggggggg"):
+    print(sched, "sync default_stream", run(sched, True, "default_stream"), flush=True)

@@ -9,6 +9,14 @@ the replay saw stale.  Each anomaly is re-run with one change before the replay:
   sync_pre    a host synchronisation between the pre-replay work and the replay
   dummy       a one-element kernel on the current stream right before the replay
   persist     the replay on one persistent non-default stream (event-ordered both ways)
+  *_nosync    the same without the host synchronisation after every step
+  all_stream  every launch of the run (eager steps, fills, capture, replays) on one
+              persistent non-default stream: nothing on the default stream
+  user_null   all_stream, plus one kernel on the default stream after every step's host
+              synchronisation (user code between the engine's steps)
+  split       eager steps and fills on one non-default stream, replays on another
+              (event-ordered), nothing on the default stream
+  capture_side  the capture issued from a non-default stream, everything else as in none
 
 Usage (one GPU): python tools/dbg/torch_replay_bisect.py
 """
@@ -95,7 +103,7 @@ def replay(graph, how):
     global _persist
     if how == "sync_pre":
         torch.cuda.synchronize()
-    elif how == "dummy":
+    elif how.startswith("dummy"):
         torch.cuda.current_stream()  # noqa: B018 (the launch below is the point)
         _dummy.add_(1)
     if how == "persist":
@@ -113,6 +121,15 @@ _dummy = torch.zeros(1, device=dev)
 
 
 def run(schedule, how, keyed):
+    if how in ("all_stream", "user_null", "split"):
+        st = torch.cuda.Stream()
+        st.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(st):
+            out = run(schedule, {"all_stream": "none", "user_null": "_user_null",
+                                 "split": "persist"}[how], keyed)
+        torch.cuda.current_stream().wait_stream(st)
+        torch.cuda.synchronize()
+        return out
     s = State()
     gen = torch.Generator(device=dev) if keyed else None
     graph, prev = None, None
@@ -123,13 +140,24 @@ def run(schedule, how, keyed):
             if graph is None or prev == "e":
                 s.step.fill_(k)
             if graph is None:
-                graph = capture(s, gen)
+                if how == "capture_side":
+                    cs = torch.cuda.Stream()
+                    cs.wait_stream(torch.cuda.current_stream())
+                    with torch.cuda.stream(cs):
+                        graph = capture(s, gen)
+                    torch.cuda.current_stream().wait_stream(cs)
+                else:
+                    graph = capture(s, gen)
                 if gen is not None:
                     gen.manual_seed(1000 + k)
             replay(graph, how)
         else:
             body(s, k, gen)
-        torch.cuda.synchronize()
+        if not how.endswith("_nosync"):
+            torch.cuda.synchronize()
+        if how == "_user_null":
+            with torch.cuda.stream(torch.cuda.default_stream()):
+                _dummy.add_(1)
         prev = mode
     torch.cuda.synchronize()
     return s
@@ -157,7 +185,9 @@ def report(name, ref, s):
 
 ref = run("e" * STEPS, "none", False)
 refk = run("e" * STEPS, "none", True)
-for how in ("none", "sync_pre", "dummy", "persist"):
+HOWS = ("none", "none_nosync", "sync_pre", "dummy", "dummy_nosync", "persist", "all_stream",
+        "user_null", "split", "capture_side")
+for how in HOWS:
     report(f"A eeeeeggggggeeeeegggg {how}", ref, run("eeeeeggggggeeeeegggg", how, False))
-for how in ("none", "sync_pre", "dummy", "persist"):
+for how in HOWS:
     report(f"B gggggggggggggggggggg {how}", refk, run("g" * STEPS, how, True))
