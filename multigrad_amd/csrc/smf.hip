@@ -405,7 +405,10 @@ struct EpiArgs {
 
 // The epilogue as the work of ONE whole workgroup of NT threads (its own kernel, or the last
 // part of the lanes fix-up launch, LMODE 2).
-template <int NB, int NT>
+// COH: the slab rows were written by other workgroups of the SAME launch (the epilogue
+// folded into the lanes forward, MG_FOLD_EPI) with device-coherent stores: read them with
+// device-coherent loads too (past this XCD's L2, which may hold none or stale lines).
+template <int NB, int NT, bool COH = false>
 __device__ __forceinline__ void epilogue_block(const EpiArgs& E, const SmfBins& bins) {
   __shared__ double scratch[NB * (NT / kWave)];
   __shared__ float Sv[kXMaxFloats];
@@ -418,13 +421,17 @@ __device__ __forceinline__ void epilogue_block(const EpiArgs& E, const SmfBins& 
   for (int k = 0; k < NB; ++k) v[k] = 0.0;
   // rows four at a time with every load issued before the first add (one memory round trip
   // per four rows instead of one per row); the per-thread order of the sums is unchanged
+  auto ld = [&](int64_t i) -> float {
+    if constexpr (COH) return __hip_atomic_load(slab + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else return slab[i];
+  };
   int r = threadIdx.x;
   for (; r + 3 * NT < nrows; r += 4 * NT) {
     float a[4][NB];
 #pragma unroll
     for (int u = 0; u < 4; ++u)
 #pragma unroll
-      for (int k = 0; k < NB; ++k) a[u][k] = slab[(int64_t)(r + u * NT) * NB + k];
+      for (int k = 0; k < NB; ++k) a[u][k] = ld((int64_t)(r + u * NT) * NB + k);
 #pragma unroll
     for (int u = 0; u < 4; ++u)
 #pragma unroll
@@ -432,7 +439,7 @@ __device__ __forceinline__ void epilogue_block(const EpiArgs& E, const SmfBins& 
   }
   for (; r < nrows; r += NT) {
 #pragma unroll
-    for (int k = 0; k < NB; ++k) v[k] += (double)slab[(int64_t)r * NB + k];
+    for (int k = 0; k < NB; ++k) v[k] += (double)ld((int64_t)r * NB + k);
   }
   block_sum_n<NB>(v, scratch);
   if (threadIdx.x == 0) {
@@ -1385,6 +1392,14 @@ __global__ __launch_bounds__(kThreads, MG_VJP_REC_MINWAVES) void smf_vjp_tiles_r
 #ifndef MG_LANES_DEFER
 #define MG_LANES_DEFER 2
 #endif
+// 1: the sumstat epilogue folded into the last workgroup of the lanes forward launch when
+// there is no fix-up launch (smf_forward_lanes); 0 (default): its own one-workgroup launch.
+// Measured alternating on one box (docs/design.md "Open performance items"): headline
+// 0.4352-0.4357 vs 0.4352-0.4364 ms/step, owner proxy 0.0626-0.0628 vs 0.0618-0.0619 --
+// the folded form is not faster, so it is compiled out by default.
+#ifndef MG_FOLD_EPI
+#define MG_FOLD_EPI 0
+#endif
 // LMODE of the main launch of the EM residual forwards (0 in builds without them)
 constexpr int kLanesMainMode =
     !(MG_FWD_EM && MG_LANES_EP) ? 0 : MG_LANES_DEFER == 1 ? 1 : MG_LANES_DEFER == 2 ? 3 : 0;
@@ -2003,9 +2018,23 @@ __global__ __launch_bounds__(kThreads, MG_LANES_MINWAVES) void smf_fwd_lanes_ker
   __shared__ float scratch[NB * (kThreads / kWave)];
   float(&bin)[NB] = *reinterpret_cast<float(*)[NB]>(acc);
   block_sum_n<NB>(bin, scratch);
+  // folded epilogue (MG_FOLD_EPI; not with the deferral list, whose fix-up launch carries
+  // it): the host passes epi.on and a self-resetting ticket in `defer`
+  constexpr bool kFoldable = MG_FOLD_EPI && LMODE != 1 && LMODE != 2;
+  const bool fold = kFoldable && epi.on;
   if (threadIdx.x == 0) {
+    if (fold) {
+      // device-coherent row stores (written through this XCD's L2), acknowledged before the
+      // ticket: no release fence, which would write back every dirty L2 line of the launch
+      // (the fused update's theta / m / v / residual stores; profiles/epilogue_in_forward/)
 #pragma unroll
-    for (int k = 0; k < NB; ++k) slab[(int64_t)blockIdx.x * NB + k] = acc[k];
+      for (int k = 0; k < NB; ++k)
+        __hip_atomic_store(slab + (int64_t)blockIdx.x * NB + k, acc[k], __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+#pragma unroll
+      for (int k = 0; k < NB; ++k) slab[(int64_t)blockIdx.x * NB + k] = acc[k];
+    }
     if constexpr (LMODE == 2) {
       // every workgroup read the count at its start; the last one to finish resets the
       // list for the next step's launch (self-resetting: graph-replay safe)
@@ -2021,6 +2050,22 @@ __global__ __launch_bounds__(kThreads, MG_LANES_MINWAVES) void smf_fwd_lanes_ker
     if (epi.on && gridDim.x == 1) {  // (the host launches the folded form with one workgroup)
       __syncthreads();
       epilogue_block<NB, kThreads>(epi, bins);
+    }
+  }
+  if constexpr (kFoldable) {
+    if (fold) {
+      // the last workgroup to finish reduces every row (its own included) and runs the
+      // epilogue: one launch per step instead of two
+      __shared__ int last_wg;
+      if (threadIdx.x == 0) {
+        uc_release();  // this workgroup's row stores acknowledged
+        last_wg = atomicAdd(defer, 1) == (int)gridDim.x - 1;
+      }
+      __syncthreads();
+      if (last_wg) {
+        if (threadIdx.x == 0) __hip_atomic_store(defer, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        epilogue_block<NB, kThreads, true>(epi, bins);
+      }
     }
   }
 }
@@ -2746,9 +2791,21 @@ int64_t smf_forward_lanes(torch::Tensor xi, torch::Tensor slot_pop, torch::Tenso
     TORCH_CHECK(epi.slab + row0 * nbp == slab.data_ptr<float>(),
                 "the chunk's slab must start at the row offset of the full slab");
   }
+  // Folded epilogue (MG_FOLD_EPI, default off): without a fix-up launch the main launch
+  // runs the epilogue in its last workgroup to finish, counted on a self-resetting ticket
+  // (`defer` holds it then: one int32, zero between launches) -- one launch per step.
+  const bool fold = MG_FOLD_EPI && with_epi && !lmode && defer.has_value() && defer->defined();
+  int* tk = nullptr;
+  if (fold) {
+    check_dev(*defer, "ticket", at::kInt);
+    TORCH_CHECK(defer->numel() >= 1, "ticket: one int32");
+    tk = defer->data_ptr<int>();
+  }
+  const EpiArgs epi_main = fold ? epi : EpiArgs{};
+  int* dmain = lmode ? dp : tk;
   auto fixup = [&]() {
     if (!lmode) {
-      if (with_epi)
+      if (with_epi && !fold)
         MG_DISPATCH_NB(nbp, {
           hipLaunchKernelGGL((smf_epilogue_kernel<NB>), dim3(1), dim3(kEpiThreads), 0, stream, epi, b);
         });
@@ -2806,20 +2863,20 @@ int64_t smf_forward_lanes(torch::Tensor xi, torch::Tensor slot_pop, torch::Tenso
                              dim3(nblocks), dim3(kThreads), 0, stream, xi.data_ptr<float>(),
                              slot_pop.data_ptr<int32_t>(), group_base.data_ptr<int64_t>(),
                              group_len.data_ptr<int32_t>(), order, tp, g0, g1, b,
-                             slab.data_ptr<float>(), rp, ws, qp, nq, u, dp);
+                             slab.data_ptr<float>(), rp, ws, qp, nq, u, dmain, epi_main);
         } else if (ledge) {
           hipLaunchKernelGGL((smf_fwd_lanes_kernel<NB, decltype(LS)::value, false, true, true, 4>),
                              dim3(nblocks), dim3(kThreads), 0, stream, xi.data_ptr<float>(),
                              slot_pop.data_ptr<int32_t>(), group_base.data_ptr<int64_t>(),
                              group_len.data_ptr<int32_t>(), order, tp, g0, g1, b,
-                             slab.data_ptr<float>(), rp, ws, qp, nq, u);
+                             slab.data_ptr<float>(), rp, ws, qp, nq, u, tk, epi_main);
         } else {
           with_bool(rel_tail, [&](auto RT) {
             hipLaunchKernelGGL((smf_fwd_lanes_kernel<NB, decltype(LS)::value, decltype(RT)::value, true, true>),
                                dim3(nblocks), dim3(kThreads), 0, stream, xi.data_ptr<float>(),
                                slot_pop.data_ptr<int32_t>(), group_base.data_ptr<int64_t>(),
                                group_len.data_ptr<int32_t>(), order, tp, g0, g1, b,
-                               slab.data_ptr<float>(), rp, ws, qp, nq, u);
+                               slab.data_ptr<float>(), rp, ws, qp, nq, u, tk, epi_main);
           });
         }
       });
@@ -2836,20 +2893,20 @@ int64_t smf_forward_lanes(torch::Tensor xi, torch::Tensor slot_pop, torch::Tenso
                            dim3(nblocks), dim3(kThreads), 0, stream, xi.data_ptr<float>(),
                            slot_pop.data_ptr<int32_t>(), group_base.data_ptr<int64_t>(),
                            group_len.data_ptr<int32_t>(), order, tp, g0, g1, b,
-                           slab.data_ptr<float>(), rp, ws, qp, nq, LanesUpdate{}, dp);
+                           slab.data_ptr<float>(), rp, ws, qp, nq, LanesUpdate{}, dmain, epi_main);
       } else if (ledge) {
         hipLaunchKernelGGL((smf_fwd_lanes_kernel<NB, decltype(LS)::value, false, true, false, 4>),
                            dim3(nblocks), dim3(kThreads), 0, stream, xi.data_ptr<float>(),
                            slot_pop.data_ptr<int32_t>(), group_base.data_ptr<int64_t>(),
                            group_len.data_ptr<int32_t>(), order, tp, g0, g1, b,
-                           slab.data_ptr<float>(), rp, ws, qp, nq);
+                           slab.data_ptr<float>(), rp, ws, qp, nq, LanesUpdate{}, tk, epi_main);
       } else {
         with_bool(rel_tail, [&](auto RT) { with_bool(has_resid, [&](auto RS) {
           hipLaunchKernelGGL((smf_fwd_lanes_kernel<NB, decltype(LS)::value, decltype(RT)::value, decltype(RS)::value>),
                              dim3(nblocks), dim3(kThreads), 0, stream, xi.data_ptr<float>(),
                              slot_pop.data_ptr<int32_t>(), group_base.data_ptr<int64_t>(),
                              group_len.data_ptr<int32_t>(), order, tp, g0, g1, b,
-                             slab.data_ptr<float>(), rp, ws, qp, nq);
+                             slab.data_ptr<float>(), rp, ws, qp, nq, LanesUpdate{}, tk, epi_main);
         }); });
       }
     });

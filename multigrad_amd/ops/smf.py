@@ -366,6 +366,14 @@ class PopulationShard:
             self._defer = torch.zeros(2 + self.ngroups, dtype=torch.int32, device=self.device)
         return self._defer
 
+    def fold_ticket(self) -> torch.Tensor:
+        """One int32 on the device, zero between launches: the workgroup-completion ticket
+        of a lanes forward that runs the sumstat epilogue in its last workgroup (csrc/smf.hip,
+        MG_FOLD_EPI; the launch resets it)."""
+        if getattr(self, "_ticket", None) is None:
+            self._ticket = torch.zeros(1, dtype=torch.int32, device=self.device)
+        return self._ticket
+
     def fwd_rows(self, nhalos: int, nbins: int = 10, log_sigma: bool = True,
                  rel_tail: bool = False, chunk: Optional[int] = None, resid: bool = True) -> int:
         """Slab rows a forward over ``chunk`` writes: the forward grid (:meth:`fwd_blocks`)
@@ -571,7 +579,8 @@ def smf_forward_slab(theta: torch.Tensor, shard: PopulationShard, bins: SmfBins,
                                        shard.group_len, shard.fwd_order, theta, list(bins.edges),
                                        list(bins.scale), bool(log_sigma), g0, g1, slab, nblk,
                                        bins.rel_tail, rbuf, w_order, w_start, queues, upd, usc,
-                                       shard.defer_buffer() if resid and lanes_fix_blocks() else None,
+                                       shard.defer_buffer() if resid and lanes_fix_blocks()
+                                       else shard.fold_ticket() if epilogue is not None else None,
                                        lanes_fix_blocks() if resid else 0, et, es, ep,
                                        bool(resid and shard.per_edge_share() >= PER_EDGE_SHARE))
         if resid:
