@@ -406,3 +406,32 @@ def test_graph_engine_replays_after_eager_steps_with_syncs(keyed):
         torch.cuda.synchronize()
     assert eng.graph is not None
     torch.testing.assert_close(eng.trajectory(), ref, rtol=1e-6, atol=1e-7)
+
+
+def test_engines_launch_on_their_own_stream():
+    """Every public engine method runs on the engine's stream (never the legacy default
+    stream; engine/_stream.py), user callbacks included, and hands the caller back a
+    stream ordered after the engine's work."""
+    from multigrad_amd.engine.fused import FusedAdamEngine
+    from multigrad_amd.engine.generic import GraphAdamEngine
+    from multigrad_amd.models.population import PopulationSMFModel, make_population_data
+    m, guess = _torch_pop(npar=2000, nhalo=40_000)
+    seen = []
+
+    def cb(i, loss, state):
+        seen.append(torch.cuda.current_stream())
+
+    eng = GraphAdamEngine(m, graph=True)
+    t = eng.run_adam(guess, nsteps=4, learning_rate=1e-3, callback=cb)
+    assert seen and all(s != torch.cuda.default_stream() for s in seen)
+    assert all(s == eng._es for s in seen)
+    assert torch.cuda.current_stream() == torch.cuda.default_stream()
+    assert torch.isfinite(t).all()
+    data = make_population_data(num_params=4000, num_halos=100_000, seed=3, device=DEV)
+    model = PopulationSMFModel(aux_data=data)
+    model.set_target_from_truth()
+    seen.clear()
+    feng = FusedAdamEngine(model, graph=False)
+    tf = feng.run_adam(data["guess"], nsteps=4, learning_rate=1e-3, callback=cb)
+    assert seen and all(s == feng._es for s in seen)
+    assert torch.isfinite(tf).all()
