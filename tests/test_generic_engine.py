@@ -168,3 +168,31 @@ def test_capture_key_attribute_probes_are_attribute_errors():
     import copy
     with pytest.raises(Exception):
         copy.copy(k).split  # protocol probes fall through to plain AttributeErrors
+
+
+def test_engine_stream_context_is_a_no_op_off_the_gpu():
+    """engine/_stream.py on a CPU engine: no stream switch, tensors handed back untouched,
+    and a decorated method's result passes through; nested contexts are fine."""
+    from multigrad_amd.engine._stream import EngineStream, on_engine_stream
+
+    class Owner:
+        calls = 0
+
+        def _engine_stream(self):
+            Owner.calls += 1
+            return None
+
+        @on_engine_stream
+        def work(self, x):
+            with EngineStream(self):
+                return {"a": [x * 2, (x + 1,)], "b": self}
+
+    o = Owner()
+    x = torch.ones(3)
+    out = o.work(x)
+    assert torch.equal(out["a"][0], 2 * x) and out["b"] is o
+    assert Owner.calls == 2
+    ctx = EngineStream(o)
+    with ctx as s:
+        assert s is None
+    ctx.hand_over([out, out])  # cycles and repeats are fine
