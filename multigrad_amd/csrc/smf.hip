@@ -2608,14 +2608,21 @@ void smf_vjp_adam_lanes(torch::Tensor slot_pop, torch::Tensor slot_part, torch::
   auto stream = at::hip::getCurrentHIPStream();
   const float2* tp = reinterpret_cast<const float2*>(theta.data_ptr<float>());
   if (s1 > s0) {
-    int dev = 0, occ = 0;
-    (void)hipGetDevice(&dev);
-    hipDeviceProp_t prop;
-    (void)hipGetDeviceProperties(&prop, dev);
-    MG_DISPATCH_NB(nbp, {
-      (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)smf_vjp_lanes_kernel<NB, true, true>, kThreads, 0);
-    });
-    const int64_t cap = (int64_t)std::max(1, occ) * prop.multiProcessorCount;
+    // resident-workgroup cap, computed once per padded bin count: the device-property and
+    // occupancy queries cost ~20 us of host time, which showed up as a gap before the
+    // pipelined engine's drain launch
+    static int64_t caps[kMaxBins + 1] = {0};
+    int64_t& cap = caps[nbp];
+    if (cap == 0) {
+      int dev = 0, occ = 0;
+      (void)hipGetDevice(&dev);
+      hipDeviceProp_t prop;
+      (void)hipGetDeviceProperties(&prop, dev);
+      MG_DISPATCH_NB(nbp, {
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)smf_vjp_lanes_kernel<NB, true, true>, kThreads, 0);
+      });
+      cap = (int64_t)std::max(1, occ) * prop.multiProcessorCount;
+    }
     const int64_t want = (s1 - s0 + kThreads - 1) / kThreads;
     const int64_t nblk = std::max<int64_t>(kXcds, std::min(cap, want) / kXcds * kXcds);
     MG_DISPATCH_NB(nbp, {
