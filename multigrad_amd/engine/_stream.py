@@ -30,15 +30,24 @@ __all__ = ["EngineStream", "on_engine_stream"]
 
 class EngineStream:
     """Context: the current stream becomes ``owner._engine_stream()`` (a no-op when that is
-    None, i.e. on the CPU, or when it is already current, i.e. nested engine calls)."""
+    None, i.e. on the CPU, or when it is already current, i.e. nested engine calls).
 
-    def __init__(self, owner):
+    ``always=False``: only while the owner may replay graphs (``owner._stream_wanted()``).
+    An engine that runs eager launches only keeps them on the caller's stream: it replays no
+    graph, and entering the engine stream costs a cross-queue event round trip per call:
+    direct ``step()`` calls on the owner-shard proxy measured 86-90 us/step of wall time and
+    49-54 us of host time with it, 64-67 and 19-21 us without (`tools/host_step_cost.py`)."""
+
+    def __init__(self, owner, always: bool = True):
         self.owner = owner
+        self.always = always
         self._ctx = None
         self._cur = None
         self._es = None
 
     def __enter__(self):
+        if not self.always and not self.owner._stream_wanted():
+            return None
         es = self.owner._engine_stream()
         if es is None:
             return None
@@ -78,16 +87,20 @@ class EngineStream:
                 todo.extend(o.values())
 
 
-def on_engine_stream(fn):
-    """Decorator: run an engine method inside :class:`EngineStream` of its engine."""
-    @functools.wraps(fn)
-    def wrapper(self, *args, **kw):
-        ctx = EngineStream(self)
-        with ctx:
-            out = fn(self, *args, **kw)
-            ctx.hand_over(out)
-        return out
-    return wrapper
+def on_engine_stream(fn=None, *, always: bool = False):
+    """Decorator: run an engine method inside :class:`EngineStream` of its engine --
+    whenever the engine may replay graphs, or (``always=True``: setup and the run drivers,
+    which capture and time graphs themselves) on every call."""
+    def deco(f):
+        @functools.wraps(f)
+        def wrapper(self, *args, **kw):
+            ctx = EngineStream(self, always=always)
+            with ctx:
+                out = f(self, *args, **kw)
+                ctx.hand_over(out)
+            return out
+        return wrapper
+    return deco(fn) if fn is not None else deco
 
 
 def make_engine_stream(current, device):

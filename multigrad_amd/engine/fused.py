@@ -203,15 +203,21 @@ class FusedAdamEngine:
                                       else self.model.param_device())
         return self._es
 
+    def _stream_wanted(self) -> bool:
+        """Launch on the engine stream while a graph may be replayed: graph mode, or any
+        captured graph still held (eager steps between replays belong there too)."""
+        return bool(getattr(self, "use_graph", False) or getattr(self, "graph", None) is not None
+                    or getattr(self, "_kgraph", None) is not None)
+
     def stream(self):
         """Context manager: the engine's own HIP stream becomes current (ordered after the
         caller's stream on entry, before it on exit).  Every public method runs its launches
         there, never on the legacy default stream (engine/_stream.py: graph replays after
         default-stream launches and a host synchronisation compute garbage on this runtime)."""
-        return EngineStream(self)
+        return EngineStream(self, always=False)
 
     # ------------------------------------------------------------------ setup
-    @on_engine_stream
+    @on_engine_stream(always=True)
     def setup(self, guess, nsteps: int, param_bounds=None, learning_rate: float = 0.01,
               b1: float = 0.9, b2: float = 0.999, eps: float = 1e-8, history="full",
               legacy_bounds_jacobian: bool = False):
@@ -1404,7 +1410,7 @@ class FusedAdamEngine:
             comm=self.comm if self.size > 1 and self.sharded else None))
 
     # ------------------------------------------------------------------ driver
-    @on_engine_stream
+    @on_engine_stream(always=True)
     def run_adam(self, guess, nsteps: int = 100, param_bounds=None, learning_rate: float = 0.01,
                  b1: float = 0.9, b2: float = 0.999, eps: float = 1e-8, history="full",
                  legacy_bounds_jacobian: bool = False, callback=None,

@@ -169,6 +169,12 @@ class GraphAdamEngine:
                                       else self.members[0].param_device())
         return self._es
 
+    def _stream_wanted(self) -> bool:
+        """Launch on the engine stream while a graph may be replayed: graph mode, or any
+        captured graph still held (eager steps between replays belong there too)."""
+        return bool(getattr(self, "use_graph", False) or getattr(self, "graph", None) is not None
+                    or getattr(self, "_kgraph", None) is not None)
+
     def stream(self):
         """Context manager: the current stream becomes the engine's own (non-default) HIP
         stream, ordered after the caller's stream on entry and before it on exit.
@@ -182,7 +188,7 @@ class GraphAdamEngine:
         (tools/dbg/torch_replay_bisect.py, torch only; docs/design.md "Graph replays and the
         default stream").  User code that calls :meth:`step` directly and launches its own
         GPU work between the calls should do that work inside ``with engine.stream():``."""
-        return EngineStream(self)
+        return EngineStream(self, always=False)
 
     # ------------------------------------------------------------------ keys
     def _next_generator(self, device) -> torch.Generator:
@@ -217,7 +223,7 @@ class GraphAdamEngine:
                 g.manual_seed(key.seed)
 
     # ------------------------------------------------------------------ setup
-    @on_engine_stream
+    @on_engine_stream(always=True)
     def setup(self, guess, nsteps: int, param_bounds=None, learning_rate: float = 0.01,
               b1: float = 0.9, b2: float = 0.999, eps: float = 1e-8, history="full",
               legacy_bounds_jacobian: bool = False, randkey=None, const_randkey: bool = False):
@@ -758,7 +764,7 @@ class GraphAdamEngine:
         t = self.history.result()[:, :self.P] if self.history.mode == "full" else self.history.result()
         return t.reshape((t.shape[0],) + self.shape)
 
-    @on_engine_stream
+    @on_engine_stream(always=True)
     def evaluator(self, x0, randkey=None):
         """``f(x) -> (loss, grad)`` replaying one captured evaluation of the distributed
         chain rule (autograd forward, sumstat all-reduce, cotangent, VJP, gradient sum):
@@ -796,7 +802,7 @@ class GraphAdamEngine:
 
         return f
 
-    @on_engine_stream
+    @on_engine_stream(always=True)
     def run_simple_grad_descent(self, guess, nsteps: int = 100, learning_rate: float = 0.01,
                                 callback=None):
         """Fixed-rate gradient descent with the reference's result contract
@@ -817,7 +823,7 @@ class GraphAdamEngine:
         self.close()
         return res
 
-    @on_engine_stream
+    @on_engine_stream(always=True)
     def run_adam(self, guess, nsteps: int = 100, param_bounds=None, learning_rate: float = 0.01,
                  b1: float = 0.9, b2: float = 0.999, eps: float = 1e-8, history="full",
                  legacy_bounds_jacobian: bool = False, callback=None, randkey=None,

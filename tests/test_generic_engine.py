@@ -182,6 +182,9 @@ def test_engine_stream_context_is_a_no_op_off_the_gpu():
             Owner.calls += 1
             return None
 
+        def _stream_wanted(self):
+            return True
+
         @on_engine_stream
         def work(self, x):
             with EngineStream(self):
