@@ -374,16 +374,18 @@ __global__ void logmse_loss_kernel(const float* __restrict__ S, const float* __r
   if (k <= nb && h) h[k] = edge_weight(g, bins, k, nb);
 }
 
-// Sumstat epilogue of one engine step in ONE launch (one 256-thread workgroup):
+// Sumstat epilogue of one engine step in ONE launch (one workgroup of MG_EPI_THREADS):
 //   slab rows -> local S (fixed-order double sums, bin scale)       [slab_reduce_kernel]
 //   -> cross-rank sum through the one-shot peer-memory exchange      [xgmi.h, size > 1]
 //   -> log-MSE loss and edge weights h (padded edges zeroed)         [logmse_loss_kernel]
 // Replaces three launches and a memset per step (~14 us on an 8-GPU owner shard).
-// One workgroup of MG_EPI_THREADS (1024 threads, one round of slab-row loads per thread,
-// measured 14.6 vs 8.0 us per launch at the headline: the wider block reduction and its
-// barriers cost more than the load round trips they save)
+// MG_EPI_THREADS: the block reduction and its barriers cost more than the extra rounds of
+// slab-row loads they save -- same-box A/B, ms/step: 1024 threads 14.6 vs 8.0 us per launch
+// at the headline (round 2); owner-shard proxy 512: 0.0644-0.0646 vs 256: 0.0622-0.0625;
+// 128: 0.0615-0.0619 vs 256: 0.0624-0.0628, headline 0.4338-0.4348 vs 0.4348-0.4375;
+// 64: 0.0617-0.0619 vs 128: 0.0615-0.0616 (round 4, tools/ab_bench_so.sh)
 #ifndef MG_EPI_THREADS
-#define MG_EPI_THREADS 256
+#define MG_EPI_THREADS 128
 #endif
 constexpr int kEpiThreads = MG_EPI_THREADS;
 
