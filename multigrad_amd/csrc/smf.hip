@@ -410,7 +410,7 @@ struct EpiArgs {
 // COH: the slab rows were written by other workgroups of the SAME launch (the epilogue
 // folded into the lanes forward, MG_FOLD_EPI) with device-coherent stores: read them with
 // device-coherent loads too (past this XCD's L2, which may hold none or stale lines).
-template <int NB, int NT, bool COH = false>
+template <int NB, int NT, bool COH = false, int U = 4>
 __device__ __forceinline__ void epilogue_block(const EpiArgs& E, const SmfBins& bins) {
   __shared__ double scratch[NB * (NT / kWave)];
   __shared__ float Sv[kXMaxFloats];
@@ -421,21 +421,22 @@ __device__ __forceinline__ void epilogue_block(const EpiArgs& E, const SmfBins& 
   double v[NB];
 #pragma unroll
   for (int k = 0; k < NB; ++k) v[k] = 0.0;
-  // rows four at a time with every load issued before the first add (one memory round trip
-  // per four rows instead of one per row); the per-thread order of the sums is unchanged
+  // rows U at a time with every load issued before the first add (one memory round trip
+  // per U rows instead of one per row); the per-thread order of the sums is the row order
+  // whatever U is (the same bits)
   auto ld = [&](int64_t i) -> float {
     if constexpr (COH) return __hip_atomic_load(slab + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     else return slab[i];
   };
   int r = threadIdx.x;
-  for (; r + 3 * NT < nrows; r += 4 * NT) {
-    float a[4][NB];
+  for (; r + (U - 1) * NT < nrows; r += U * NT) {
+    float a[U][NB];
 #pragma unroll
-    for (int u = 0; u < 4; ++u)
+    for (int u = 0; u < U; ++u)
 #pragma unroll
       for (int k = 0; k < NB; ++k) a[u][k] = ld((int64_t)(r + u * NT) * NB + k);
 #pragma unroll
-    for (int u = 0; u < 4; ++u)
+    for (int u = 0; u < U; ++u)
 #pragma unroll
       for (int k = 0; k < NB; ++k) v[k] += (double)a[u][k];
   }
@@ -470,9 +471,16 @@ __device__ __forceinline__ void epilogue_block(const EpiArgs& E, const SmfBins& 
   if (E.advance != nullptr && threadIdx.x == 0) E.advance[0] += 1;
 }
 
+// Rows per load round of the stand-alone epilogue: MG_EPI_UNROLL rows of NB floats in
+// flight per thread.  16 measured slower than 4 (owner proxy 0.0620-0.0623 vs 0.0609-0.0614
+// ms/step, same-box A/B, round 4)
+#ifndef MG_EPI_UNROLL
+#define MG_EPI_UNROLL 4
+#endif
+
 template <int NB>
 __global__ __launch_bounds__(kEpiThreads) void smf_epilogue_kernel(EpiArgs E, SmfBins bins) {
-  epilogue_block<NB, kEpiThreads>(E, bins);
+  epilogue_block<NB, kEpiThreads, false, MG_EPI_UNROLL>(E, bins);
 }
 
 // Per-halo VJP contributions in the scaled coordinate w = z*kWScale:
