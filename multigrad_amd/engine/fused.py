@@ -687,7 +687,7 @@ class FusedAdamEngine:
         apply(cands[best])
         self.tuning = {"candidates": [dict(c, ms=round(1e3 * t, 4) if math.isfinite(t) else None)
                                       for c, t in zip(cands, times)],
-                       "chosen": cands[best], "steps_per_window": reps}
+                       "chosen": cands[best], "steps_per_window": reps, "rounds": rounds}
         if dropped:
             self.tuning["dropped"] = dropped
         if self.use_graph:
