@@ -410,6 +410,12 @@ struct EpiArgs {
 // COH: the slab rows were written by other workgroups of the SAME launch (the epilogue
 // folded into the lanes forward, MG_FOLD_EPI) with device-coherent stores: read them with
 // device-coherent loads too (past this XCD's L2, which may hold none or stale lines).
+// 1: the stand-alone epilogue reduces the slab as a flat array with coalesced loads (see
+// epilogue_block); 0: row by row
+#ifndef MG_EPI_FLAT
+#define MG_EPI_FLAT 0
+#endif
+
 template <int NB, int NT, bool COH = false, int U = 4>
 __device__ __forceinline__ void epilogue_block(const EpiArgs& E, const SmfBins& bins) {
   __shared__ double scratch[NB * (NT / kWave)];
@@ -418,36 +424,68 @@ __device__ __forceinline__ void epilogue_block(const EpiArgs& E, const SmfBins& 
   __shared__ float d2[kMaxBins];
   const float* __restrict__ slab = E.slab;
   const int nrows = E.nrows, nb = E.nb;
-  double v[NB];
+  if constexpr (MG_EPI_FLAT && !COH) {
+    // the slab as one flat float array: NT / NB row groups of NB threads, thread t always
+    // on bin t % NB, so every load instruction of a wave reads contiguous floats (the row
+    // form reads 64 rows 40 bytes apart); per-thread sums in element order, then the row
+    // groups of each bin in a fixed order (deterministic)
+    constexpr int G = NT / NB;
+    constexpr int TA = G * NB;
+    constexpr int UF = 16;
+    __shared__ double part[NT];
+    const int t = threadIdx.x;
+    double acc = 0.0;
+    if (t < TA) {
+      const int64_t L = (int64_t)nrows * NB;
+      int64_t i = t;
+      for (; i + (int64_t)(UF - 1) * TA < L; i += (int64_t)UF * TA) {
+        float a[UF];
 #pragma unroll
-  for (int k = 0; k < NB; ++k) v[k] = 0.0;
-  // rows U at a time with every load issued before the first add (one memory round trip
-  // per U rows instead of one per row); the per-thread order of the sums is the row order
-  // whatever U is (the same bits)
-  auto ld = [&](int64_t i) -> float {
-    if constexpr (COH) return __hip_atomic_load(slab + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    else return slab[i];
-  };
-  int r = threadIdx.x;
-  for (; r + (U - 1) * NT < nrows; r += U * NT) {
-    float a[U][NB];
+        for (int u = 0; u < UF; ++u) a[u] = slab[i + (int64_t)u * TA];
 #pragma unroll
-    for (int u = 0; u < U; ++u)
+        for (int u = 0; u < UF; ++u) acc += (double)a[u];
+      }
+      for (; i < L; i += TA) acc += (double)slab[i];
+    }
+    part[t] = acc;
+    __syncthreads();
+    if (t < NB) {
+      double sum = 0.0;
+      for (int m = 0; m < G; ++m) sum += part[m * NB + t];
+      Sv[t] = (float)(sum * (double)bins.scale[t]);
+    }
+  } else {
+    double v[NB];
 #pragma unroll
-      for (int k = 0; k < NB; ++k) a[u][k] = ld((int64_t)(r + u * NT) * NB + k);
+    for (int k = 0; k < NB; ++k) v[k] = 0.0;
+    // rows U at a time with every load issued before the first add (one memory round trip
+    // per U rows instead of one per row); the per-thread order of the sums is the row order
+    // whatever U is (the same bits)
+    auto ld = [&](int64_t i) -> float {
+      if constexpr (COH) return __hip_atomic_load(slab + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      else return slab[i];
+    };
+    int r = threadIdx.x;
+    for (; r + (U - 1) * NT < nrows; r += U * NT) {
+      float a[U][NB];
 #pragma unroll
-    for (int u = 0; u < U; ++u)
+      for (int u = 0; u < U; ++u)
 #pragma unroll
-      for (int k = 0; k < NB; ++k) v[k] += (double)a[u][k];
-  }
-  for (; r < nrows; r += NT) {
+        for (int k = 0; k < NB; ++k) a[u][k] = ld((int64_t)(r + u * NT) * NB + k);
 #pragma unroll
-    for (int k = 0; k < NB; ++k) v[k] += (double)ld((int64_t)r * NB + k);
-  }
-  block_sum_n<NB>(v, scratch);
-  if (threadIdx.x == 0) {
+      for (int u = 0; u < U; ++u)
 #pragma unroll
-    for (int k = 0; k < NB; ++k) Sv[k] = (float)(v[k] * (double)bins.scale[k]);
+        for (int k = 0; k < NB; ++k) v[k] += (double)a[u][k];
+    }
+    for (; r < nrows; r += NT) {
+#pragma unroll
+      for (int k = 0; k < NB; ++k) v[k] += (double)ld((int64_t)r * NB + k);
+    }
+    block_sum_n<NB>(v, scratch);
+    if (threadIdx.x == 0) {
+#pragma unroll
+      for (int k = 0; k < NB; ++k) Sv[k] = (float)(v[k] * (double)bins.scale[k]);
+    }
   }
   __syncthreads();
   if (E.size > 1) xgmi_block_allreduce(E.peers, E.rank, E.size, Sv, NB, E.seq, E.err, E.ticks);
