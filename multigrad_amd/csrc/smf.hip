@@ -411,7 +411,8 @@ struct EpiArgs {
 // folded into the lanes forward, MG_FOLD_EPI) with device-coherent stores: read them with
 // device-coherent loads too (past this XCD's L2, which may hold none or stale lines).
 // 1: the stand-alone epilogue reduces the slab as a flat array with coalesced loads (see
-// epilogue_block); 0: row by row
+// epilogue_block); 0: row by row.  Same-box A/B (round 4, profiles/knobs_r4/): within the
+// run-to-run spread on the owner proxy and the headline, so the row form stays
 #ifndef MG_EPI_FLAT
 #define MG_EPI_FLAT 0
 #endif
