@@ -88,7 +88,8 @@ def lbfgs(comm, iters, params, halos):
     dt = time.perf_counter() - t0
     return {"config": f"lbfgs-{params:.0e}param", "value": res.nit / dt, "unit": "iterations/s",
             "fevals_per_s": res.nfev / dt, "n_ranks": comm.size, "nit": int(res.nit),
-            "nfev": int(res.nfev), "fun": float(res.fun), "sharded": bool(obj.sharded)}
+            "nfev": int(res.nfev), "fun": float(res.fun), "sharded": bool(obj.sharded),
+            "reduction": res.get("reduction"), "host_collectives": res.get("host_collectives")}
 
 
 def lbfgsb(comm, iters, params, halos):
@@ -119,7 +120,8 @@ def lbfgsb(comm, iters, params, halos):
     dt = time.perf_counter() - t0
     return {"config": f"lbfgsb-{params:.0e}param", "value": res.nit / dt, "unit": "iterations/s",
             "fevals_per_s": res.nfev / dt, "n_ranks": comm.size, "nit": int(res.nit),
-            "nfev": int(res.nfev), "fun": float(res.fun), "sharded": bool(obj.sharded)}
+            "nfev": int(res.nfev), "fun": float(res.fun), "sharded": bool(obj.sharded),
+            "reduction": res.get("reduction"), "host_collectives": res.get("host_collectives")}
 
 
 def main(argv=None):

@@ -91,6 +91,10 @@ void xgmi_zero(int64_t base, int64_t bytes);
 void xgmi_free(int64_t ptr);
 void xgmi_allreduce(torch::Tensor x, std::vector<int64_t> peers, int64_t rank, torch::Tensor seq,
                     torch::Tensor err, double timeout_s);
+void xgmi_allreduce_wide(torch::Tensor x, int64_t nsum, int64_t nmax, std::vector<int64_t> peers,
+                         int64_t rank, torch::Tensor seq, torch::Tensor err, double timeout_s);
+int64_t xgmi_wide_region_bytes();
+std::string device_pci_bus_id();
 // adam.hip
 void fused_adam(torch::Tensor u, torch::Tensor m, torch::Tensor v, torch::Tensor g,
                 c10::optional<torch::Tensor> p, c10::optional<torch::Tensor> lo,
@@ -183,6 +187,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("xgmi_zero", &mg::xgmi_zero, pybind11::arg("base"), pybind11::arg("bytes") = 0);
   m.def("xgmi_free", &mg::xgmi_free);
   m.def("xgmi_allreduce", &mg::xgmi_allreduce);
+  m.def("xgmi_allreduce_wide", &mg::xgmi_allreduce_wide);
+  m.def("xgmi_wide_region_bytes", &mg::xgmi_wide_region_bytes);
+  m.def("device_pci_bus_id", &mg::device_pci_bus_id);
   m.def("fused_adam", &mg::fused_adam, pybind11::arg("u"), pybind11::arg("m"), pybind11::arg("v"),
         pybind11::arg("g"), pybind11::arg("p"), pybind11::arg("lo"), pybind11::arg("hi"),
         pybind11::arg("kind"), pybind11::arg("step"), pybind11::arg("lr"), pybind11::arg("b1"),

@@ -39,7 +39,10 @@ namespace mg {
 constexpr int kMaxBins = 32;
 constexpr int kXcds = 8;  // MI355X: 8 XCDs (L2 domains), workgroups dispatched round-robin
 constexpr int kThreads = 256;
-constexpr int kItems = 8;                       // halos per thread in a tile
+// the fused exchange runs twoshot_block (grid-stride by kTsThreads) inside launches of
+// kThreads threads: a mismatch would skip or double-update parameters
+static_assert(kThreads == kTsThreads, "fused-exchange kernels must launch kTsThreads threads");
+constexpr int kItems = 8;                      // halos per thread in a tile
 constexpr int kTileHalos = kThreads * kItems;   // 2048
 constexpr int kTilePops = 2048;
 constexpr float kLn10 = 2.302585092994046f;

@@ -40,15 +40,23 @@ struct TwoShotArgs {
 constexpr int kTsThreads = 256;
 
 // MODE 0: plain sum (self-test: theta = sum of the gradients); 1: Adam, unbounded;
-// 2: Adam in bounded coordinates; 3: bounded with the reference's legacy Jacobian (Q1).
+// 2: Adam in bounded coordinates; 3: bounded with the reference's legacy Jacobian (Q1);
+// 4: reduce-scatter only -- the rank-order sum of the owned slice goes to the local buffer
+// `u`, nothing is pushed; 5: all-gather only -- the local slice `u` is pushed into every
+// rank's parameter region, nothing is pulled.  (4 and 5 are the device L-BFGS's sharded
+// evaluation: gradient to the owned slice, owned slice of the iterate to every rank.)
 // The exchange as workgroups [0, nblk) of the calling grid (bid = this workgroup's index in
 // that range).  Every workgroup of the range must call it; it returns when this
 // workgroup's share is done (the last one returns when every rank's slice has landed).
 template <int MODE, int PB = kXMaxRanks>
 __device__ __forceinline__ void twoshot_block(const TwoShotArgs& a, int bid, int nblk) {
   static_assert(kXMaxRanks % PB == 0, "peer batches must tile the rank limit");
-  constexpr bool BOUNDED = MODE >= 2;
+  static_assert(MODE >= 0 && MODE <= 5, "two-shot mode");
+  constexpr bool ADAM = MODE >= 1 && MODE <= 3;
+  constexpr bool BOUNDED = MODE == 2 || MODE == 3;
   constexpr bool LEGACY = MODE == 3;
+  constexpr bool PULL = MODE != 5;
+  constexpr bool PUSH = MODE != 4;
   const unsigned seq = __hip_atomic_load(a.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
   const int st = a.host_step >= 0
                      ? a.host_step
@@ -72,24 +80,28 @@ __device__ __forceinline__ void twoshot_block(const TwoShotArgs& a, int bid, int
     // PB = 8: every load in flight (the stand-alone kernel); PB = 4 keeps the registers of
     // the compute kernels that carry the exchange (fused exchange)
     float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
+    if constexpr (PULL) {
 #pragma unroll
-    for (int q0 = 0; q0 < kXMaxRanks; q0 += PB) {
-      float4 hs[PB];
+      for (int q0 = 0; q0 < kXMaxRanks; q0 += PB) {
+        float4 hs[PB];
 #pragma unroll
-      for (int j = 0; j < PB; ++j)
-        if (q0 + j < a.size)
-          hs[j] = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(a.g.base[q0 + j]) + off);
+        for (int j = 0; j < PB; ++j)
+          if (q0 + j < a.size)
+            hs[j] = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(a.g.base[q0 + j]) + off);
 #pragma unroll
-      for (int j = 0; j < PB; ++j) {
-        if (q0 + j == 0) {
-          g = hs[0];
-        } else if (q0 + j < a.size) {
-          g.x += hs[j].x; g.y += hs[j].y; g.z += hs[j].z; g.w += hs[j].w;
+        for (int j = 0; j < PB; ++j) {
+          if (q0 + j == 0) {
+            g = hs[0];
+          } else if (q0 + j < a.size) {
+            g.x += hs[j].x; g.y += hs[j].y; g.z += hs[j].z; g.w += hs[j].w;
+          }
         }
       }
+    } else {
+      g = reinterpret_cast<const float4*>(a.u)[i];
     }
     float4 p = g;
-    if constexpr (MODE >= 1) {
+    if constexpr (ADAM) {
       float4 u = BOUNDED ? reinterpret_cast<const float4*>(a.u)[i]
                          : reinterpret_cast<const float4*>(own)[i];
       float4 m = reinterpret_cast<const float4*>(a.m)[i];
@@ -119,8 +131,11 @@ __device__ __forceinline__ void twoshot_block(const TwoShotArgs& a, int bid, int
       const float nan = __builtin_nanf("");
       p = make_float4(nan, nan, nan, nan);
     }
-    for (int q = 0; q < a.size; ++q)
-      *reinterpret_cast<float4*>(reinterpret_cast<float*>(a.t.base[q]) + off) = p;
+    if constexpr (MODE == 4) reinterpret_cast<float4*>(a.u)[i] = p;
+    if constexpr (PUSH) {
+      for (int q = 0; q < a.size; ++q)
+        *reinterpret_cast<float4*>(reinterpret_cast<float*>(a.t.base[q]) + off) = p;
+    }
   }
   // grid completion: every thread's pushes are acknowledged before its block takes a
   // ticket; the last block publishes "my slice is everywhere" and waits until every

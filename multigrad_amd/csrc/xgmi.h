@@ -99,6 +99,29 @@ __device__ __forceinline__ void xgmi_block_allreduce(const XgmiPeers& peers, int
 
 namespace mg {
 
+// ---------------------------------------------------------------------------- wide one-shot
+// The same push / signal / poll / local-sum protocol for the optimizers' reductions (device
+// L-BFGS(-B): the packed inner products of an iteration, the directional derivative of a
+// line-search point): up to kXwMax fp64 values per call, values [0, nsum) summed and
+// [nsum, nsum + nmax) max-reduced, both in rank order, so every rank holds the same bits.
+// Values travel as raw 64-bit words (no fp32 rounding anywhere on the way).
+constexpr int kXwMax = 1024;
+constexpr int kXwThreads = 256;
+constexpr int kXwFlagOff = 0;       // uint32 flags[2][kXMaxRanks]
+constexpr int kXwDataOff = 256;     // uint64 data[2][kXMaxRanks][kXwMax]
+constexpr int64_t kXwRegionBytes = kXwDataOff + 2LL * kXMaxRanks * kXwMax * 8;
+
+__device__ __forceinline__ unsigned* xwflags(char* b) {
+  return reinterpret_cast<unsigned*>(b + kXwFlagOff);
+}
+__device__ __forceinline__ unsigned long long* xwdata(char* b) {
+  return reinterpret_cast<unsigned long long*>(b + kXwDataOff);
+}
+
+}  // namespace mg
+
+namespace mg {
+
 // ---------------------------------------------------------------------------- two-shot
 // Flag region of the two-shot reduce-scatter / all-gather (one per rank, uncached, IPC
 // mapped by every peer): gflag[q] = last step whose gradient rank q has published,

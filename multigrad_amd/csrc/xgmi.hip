@@ -47,6 +47,60 @@ __global__ __launch_bounds__(64) void xgmi_oneshot_kernel(XgmiPeers peers, int r
   if (threadIdx.x < n) x[threadIdx.x] = v[threadIdx.x];
 }
 
+// Wide one-shot (xgmi.h): in-place all-reduce of x[0, nsum + nmax) fp64, [0, nsum) summed
+// and the rest max-reduced, in rank order.  One workgroup; the protocol (two slots, the
+// sequence number in device memory, bounded waits that NaN-poison the result) is the one of
+// xgmi_oneshot_kernel.
+__global__ __launch_bounds__(kXwThreads) void xgmi_oneshot_wide_kernel(
+    XgmiPeers peers, int rank, int size, double* __restrict__ x, int nsum, int nmax,
+    unsigned* __restrict__ seq_ptr, int* __restrict__ err, long long timeout_ticks) {
+  const int t = threadIdx.x;
+  const int n = nsum + nmax;
+  const unsigned seq = *seq_ptr + 1u;
+  const int slot = (int)(seq & 1u);
+  for (int i = t; i < n; i += kXwThreads) {
+    const unsigned long long bits = (unsigned long long)__double_as_longlong(x[i]);
+    for (int p = 0; p < size; ++p)
+      __hip_atomic_store(xwdata(peers.base[p]) + (int64_t)(slot * kXMaxRanks + rank) * kXwMax + i,
+                         bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  uc_release();
+  __syncthreads();
+  if (t < size) uc_signal(xwflags(peers.base[t]) + slot * kXMaxRanks + rank, seq);
+  char* me = peers.base[rank];
+  __shared__ int timed_out;
+  if (t == 0) timed_out = 0;
+  __syncthreads();
+  if (t < size) {
+    const long long t0 = wall_clock64();
+    const bool dead = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+    while (uc_poll(xwflags(me) + slot * kXMaxRanks + t) != seq) {
+      if (dead || wall_clock64() - t0 > timeout_ticks) {
+        atomicExch(err, 1);
+        timed_out = 1;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+  }
+  asm volatile("" ::: "memory");
+  __syncthreads();
+  for (int i = t; i < n; i += kXwThreads) {
+    double s = 0.0;
+    for (int q = 0; q < size; ++q) {
+      const double v = __longlong_as_double((long long)__hip_atomic_load(
+          xwdata(me) + (int64_t)(slot * kXMaxRanks + q) * kXwMax + i, __ATOMIC_RELAXED,
+          __HIP_MEMORY_SCOPE_SYSTEM));
+      if (q == 0) s = v;
+      else if (i < nsum) s += v;
+      else s = v > s ? v : s;
+    }
+    x[i] = timed_out ? __builtin_nan("") : s;
+  }
+  __syncthreads();
+  if (t == 0) *seq_ptr = seq;
+}
+
 static void xcheck(hipError_t e, const char* what) {
   TORCH_CHECK(e == hipSuccess, what, ": ", hipGetErrorString(e));
 }
@@ -117,6 +171,40 @@ void xgmi_allreduce(torch::Tensor x, std::vector<int64_t> peers, int64_t rank, t
                      reinterpret_cast<unsigned*>(seq.data_ptr<int>()), err.data_ptr<int>(), ticks);
 }
 
+// In-place fp64 all-reduce of x[0, nsum + nmax) over the ranks of `peers` (wide one-shot
+// regions, xgmi_alloc(xgmi_wide_region_bytes())): [0, nsum) summed, the rest max-reduced.
+void xgmi_allreduce_wide(torch::Tensor x, int64_t nsum, int64_t nmax, std::vector<int64_t> peers,
+                         int64_t rank, torch::Tensor seq, torch::Tensor err, double timeout_s) {
+  TORCH_CHECK(x.is_cuda() && x.is_contiguous() && x.scalar_type() == at::kDouble,
+              "x: contiguous fp64 device");
+  TORCH_CHECK(nsum >= 0 && nmax >= 0 && nsum + nmax >= 1 && nsum + nmax <= kXwMax &&
+              nsum + nmax <= x.numel(), "wide one-shot all-reduce takes 1..1024 values");
+  const int size = (int)peers.size();
+  TORCH_CHECK(size >= 1 && size <= kXMaxRanks && rank >= 0 && rank < size, "bad rank/size");
+  TORCH_CHECK(seq.is_cuda() && seq.scalar_type() == at::kInt && err.is_cuda() &&
+              err.scalar_type() == at::kInt, "seq/err: int32 device");
+  XgmiPeers p;
+  for (int r = 0; r < kXMaxRanks; ++r) p.base[r] = r < size ? reinterpret_cast<char*>(peers[r]) : nullptr;
+  const long long ticks = (long long)(timeout_s * 1e8);
+  hipLaunchKernelGGL(xgmi_oneshot_wide_kernel, dim3(1), dim3(kXwThreads), 0,
+                     at::hip::getCurrentHIPStream(), p, (int)rank, size, x.data_ptr<double>(),
+                     (int)nsum, (int)nmax, reinterpret_cast<unsigned*>(seq.data_ptr<int>()),
+                     err.data_ptr<int>(), ticks);
+}
+
+int64_t xgmi_wide_region_bytes() { return kXwRegionBytes; }
+
+// PCI bus id of the current device: ranks that report the same id (and host) share one GPU
+// and size their peer-memory exchange grids so that every rank's exchange workgroups can
+// be resident at once (parallel/xgmi.py).
+std::string device_pci_bus_id() {
+  int dev = 0;
+  xcheck(hipGetDevice(&dev), "hipGetDevice");
+  char buf[64] = {0};
+  xcheck(hipDeviceGetPCIBusId(buf, (int)sizeof(buf) - 1, dev), "hipDeviceGetPCIBusId");
+  return std::string(buf);
+}
+
 
 // ============================================================================ two-shot
 // Reduce-scatter -> Adam -> all-gather of the dense gradient over peer memory, ONE launch
@@ -167,7 +255,7 @@ static float* opt_ptr(const c10::optional<torch::Tensor>& t, int64_t numel, cons
 }
 
 // Launch arguments of one two-shot step (see above).  mode: 0 sum, 1 Adam, 2 bounded
-// Adam, 3 bounded legacy.  scalars: [host_step, lr, b1, b2, eps, timeout_s, traj_stride
+// Adam, 3 bounded legacy, 4 reduce-scatter into u, 5 all-gather of u (twoshot.h).  scalars: [host_step, lr, b1, b2, eps, timeout_s, traj_stride
 // (, max_blocks)]; returns the packed arguments with the mode and the workgroup count.
 static TwoShotPack twoshot_args(std::vector<int64_t> gbufs, std::vector<int64_t> tbufs,
                                 std::vector<int64_t> flags, int64_t rank, int64_t lo, int64_t n,
@@ -183,7 +271,7 @@ static TwoShotPack twoshot_args(std::vector<int64_t> gbufs, std::vector<int64_t>
   TORCH_CHECK(rank >= 0 && rank < size, "bad rank");
   TORCH_CHECK(lo >= 0 && n >= 0 && lo % 4 == 0 && n % 4 == 0 && lo + n <= total,
               "owned range must be float4 aligned and inside the vector");
-  TORCH_CHECK(mode >= 0 && mode <= 3, "bad mode");
+  TORCH_CHECK(mode >= 0 && mode <= 5, "bad mode");
   TORCH_CHECK(scalars.size() == 7 || scalars.size() == 8,
               "scalars: host_step, lr, b1, b2, eps, timeout_s, traj_stride[, max_blocks]");
   TORCH_CHECK(step.is_cuda() && step.scalar_type() == at::kInt && step.numel() >= 2, "step: [2] int32 device");
@@ -212,8 +300,10 @@ static TwoShotPack twoshot_args(std::vector<int64_t> gbufs, std::vector<int64_t>
   a.traj = opt_ptr(traj, -1, "traj");
   a.traj_stride = (int64_t)scalars[6];
   TORCH_CHECK(a.traj_stride % 4 == 0, "trajectory stride must keep float4 alignment");
-  if (mode >= 1) TORCH_CHECK(a.m && a.v, "Adam modes need m and v");
-  if (mode >= 2) TORCH_CHECK(a.u && a.blo && a.bhi && a.kind, "bounded modes need u and the bounds");
+  if (mode >= 1 && mode <= 3) TORCH_CHECK(a.m && a.v, "Adam modes need m and v");
+  if (mode == 2 || mode == 3)
+    TORCH_CHECK(a.u && a.blo && a.bhi && a.kind, "bounded modes need u and the bounds");
+  if (mode >= 4) TORCH_CHECK(a.u, "reduce-scatter / all-gather modes need the local slice u");
   a.step = step.data_ptr<int>();
   a.host_step = (int)scalars[0];
   a.lr = (float)scalars[1];
@@ -250,7 +340,9 @@ void twoshot_launch(const TwoShotPack& P, hipStream_t stream) {
     case 0: hipLaunchKernelGGL(xgmi_twoshot_kernel<0>, dim3(P.blocks), dim3(kTsThreads), 0, stream, P.a); break;
     case 1: hipLaunchKernelGGL(xgmi_twoshot_kernel<1>, dim3(P.blocks), dim3(kTsThreads), 0, stream, P.a); break;
     case 2: hipLaunchKernelGGL(xgmi_twoshot_kernel<2>, dim3(P.blocks), dim3(kTsThreads), 0, stream, P.a); break;
-    default: hipLaunchKernelGGL(xgmi_twoshot_kernel<3>, dim3(P.blocks), dim3(kTsThreads), 0, stream, P.a); break;
+    case 3: hipLaunchKernelGGL(xgmi_twoshot_kernel<3>, dim3(P.blocks), dim3(kTsThreads), 0, stream, P.a); break;
+    case 4: hipLaunchKernelGGL(xgmi_twoshot_kernel<4>, dim3(P.blocks), dim3(kTsThreads), 0, stream, P.a); break;
+    default: hipLaunchKernelGGL(xgmi_twoshot_kernel<5>, dim3(P.blocks), dim3(kTsThreads), 0, stream, P.a); break;
   }
 }
 
@@ -271,7 +363,7 @@ pybind11::bytes xgmi_twoshot_pack(std::vector<int64_t> gbufs, std::vector<int64_
                                   c10::optional<torch::Tensor> kind, c10::optional<torch::Tensor> traj,
                                   torch::Tensor step, torch::Tensor seq, torch::Tensor err,
                                   std::vector<double> scalars) {
-  TORCH_CHECK(mode >= 1, "a fused exchange is an Adam step (mode 1..3)");
+  TORCH_CHECK(mode >= 1 && mode <= 3, "a fused exchange is an Adam step (mode 1..3)");
   const TwoShotPack P = twoshot_args(gbufs, tbufs, flags, rank, lo, n, total, mode, u, m, v, blo,
                                      bhi, kind, traj, step, seq, err, scalars);
   return pybind11::bytes(reinterpret_cast<const char*>(&P), sizeof(P));

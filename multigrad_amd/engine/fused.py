@@ -1455,7 +1455,13 @@ class _EngineObjective:
     ZeRO (world > 1): x is the concatenation of this rank's slices of every chunk; an
     evaluation all-gathers the chunks, runs forward + loss + per-chunk VJP, and
     reduce-scatters the gradient back to the owned slices -- L-BFGS vectors and history
-    are sharded 1/W and its dot products are all-reduced by the optimizer.
+    are sharded 1/W and its dot products are all-reduced by the optimizer.  With the
+    two-shot peer-memory context up, the all-gather is its mode 5 (each rank pushes its
+    slices into every rank's parameter region) and the reduce-scatter its mode 4 (rank-order
+    sum of the owned slices of every rank's gradient region): the evaluation makes no RCCL
+    or host collective.  Otherwise RCCL reduce-scatter / all-gather on the same layout.
+    Owner placement: x is the owned parameter range, whose gradient is complete locally
+    (only the sumstats cross ranks, inside the forward's epilogue).
     Replicated: x is the full (padded) parameter vector and the gradient is all-reduced.
     """
 
@@ -1464,6 +1470,7 @@ class _EngineObjective:
         self.comm = eng.comm
         self.sharded = eng.zero or eng.owner
         self.device = eng.device
+        self.ts = eng.twoshot if (eng.zero and not eng.owner) else None
         if eng.owner:
             self.n_local = eng.own_range[1] - eng.own_range[0]
         else:
@@ -1510,6 +1517,11 @@ class _EngineObjective:
         for c in range(e.C):
             a, b = e.own[c]
             o, n = e.loc_off[c], e.loc_len[c]
+            if self.ts is not None:
+                # this rank's slice into every rank's parameter region (its own included);
+                # the launch returns when every rank's slice of the chunk has landed here
+                self.ts.all_gather_(x[o:o + n], a, n)
+                continue
             e.theta[a:b].copy_(x[o:o + n])
             pa, L = e.pb[c], e.lengths[c]
             agc = e.comm_ag if e.comm_ag is not None else e.comm
@@ -1531,6 +1543,13 @@ class _EngineObjective:
             md.engine_vjp_into(e.theta, e.h, e.grad, chunk=e.rank)
             a, b = e.own_range
             g = e.grad[a:b]
+        elif e.zero and self.ts is not None:
+            for c in range(e.C):
+                md.engine_vjp_into(e.theta, e.h, e.grad, chunk=c)
+                a, b = e.own[c]
+                o, n = e.loc_off[c], e.loc_len[c]
+                self.ts.reduce_scatter_(e.g_loc[o:o + n], a, n)
+            g = e.g_loc
         elif e.zero:
             works = []
             for c in range(e.C):

@@ -35,6 +35,7 @@ import scipy.optimize
 import torch
 
 from ..ops.lbfgs import MultiDot, lincomb_
+from ._reduce import DeviceReducer
 
 __all__ = ["lbfgs_minimize", "GenericObjective", "run_lbfgs_device"]
 
@@ -75,14 +76,6 @@ class GenericObjective:
         return float(torch.as_tensor(loss).detach().double()), g.contiguous()
 
 
-def _allreduce_np(comm, arr: np.ndarray, op="sum", sharded=True) -> np.ndarray:
-    if comm is None or comm.size == 1 or not sharded:
-        return arr
-    t = torch.from_numpy(np.ascontiguousarray(arr, dtype=np.float64))
-    comm.all_reduce(t, op=op)
-    return t.numpy()
-
-
 def _cubic_min(a, fa, da, b, fb, db):
     """Minimiser of the cubic interpolating (a, fa, da), (b, fb, db) (None if degenerate)."""
     d1 = da + db - 3 * (fa - fb) / (a - b)
@@ -99,10 +92,17 @@ def _cubic_min(a, fa, da, b, fb, db):
 def _lbfgs_minimize_impl(obj, maxiter: int = 100, m: int = 10, ftol: float = 1e7 * _EPS,
                    gtol: float = 1e-5, maxls: int = 20, c1: float = 1e-4, c2: float = 0.9,
                    callback=None) -> scipy.optimize.OptimizeResult:
-    """Minimise ``obj`` (see :class:`GenericObjective`) with L-BFGS; SPMD-consistent."""
+    """Minimise ``obj`` (see :class:`GenericObjective`) with L-BFGS; SPMD-consistent.
+
+    Every cross-rank reduction of the loop runs on the devices (:class:`DeviceReducer`:
+    the wide one-shot peer-memory kernel, else RCCL) and comes back in one device->host copy:
+    one per iteration (the dot block with max|g|) and one per line-search evaluation (the
+    loss with the directional derivative).  The result records the host collectives the
+    iterations made (``host_collectives``; 0 on GPUs)."""
     comm, sharded = obj.comm, obj.sharded
     n = obj.n_local
     dev = obj.device
+    red = DeviceReducer(comm, sharded, dev)  # collective (may connect peer memory)
     x = obj.x0().contiguous()
     f, g = obj(x)
     g = g.clone()  # the objective may return a view of a buffer the next evaluation reuses
@@ -110,8 +110,8 @@ def _lbfgs_minimize_impl(obj, maxiter: int = 100, m: int = 10, ftol: float = 1e7
     # rows 0..2m-1: the S and Y slots; 2m, 2m+1: the new pair s, y; 2m+2: the new gradient.
     # One multi-dot of all rows against (s, y, g) gives every scalar an iteration needs
     # (s.y, y.y, the new Gram rows, S^T g, Y^T g, g.g), and max|g| rides along in the same
-    # device->host copy: with the line search's one copy per evaluation, a typical
-    # iteration makes two.
+    # reduction and device->host copy: with the line search's one copy per evaluation, a
+    # typical iteration makes two.
     HX = torch.zeros((2 * m + 3, n), dtype=torch.float32, device=dev)
     HS = HX[:2 * m]
     s_vec, y_vec, g_row = HX[2 * m], HX[2 * m + 1], HX[2 * m + 2]
@@ -126,25 +126,22 @@ def _lbfgs_minimize_impl(obj, maxiter: int = 100, m: int = 10, ftol: float = 1e7
     xt = torch.empty_like(x)
     dev_call = getattr(obj, "device_call", None) if dev.type == "cuda" else None
     coef = torch.zeros(2 * m, dtype=torch.float32, device=dev)
-    gmax_dev = torch.zeros(1, dtype=torch.float64, device=dev)
 
-    def gdot(a: torch.Tensor, b: torch.Tensor) -> float:
-        v = dot1(a.view(1, -1), 1, [b]).cpu().numpy().reshape(-1)
-        return float(_allreduce_np(comm, v, sharded=sharded)[0])
+    def absmax(gv: torch.Tensor) -> torch.Tensor:
+        return gv.abs().max().double() if gv.numel() else torch.zeros((), dtype=torch.float64,
+                                                                     device=gv.device)
 
     def gstats(gv: torch.Tensor):
         """(global g.g, global max|g|) in one copy."""
-        gg_loc = dot1(gv.view(1, -1), 1, [gv]).reshape(1)
-        gmax_dev.copy_(gv.abs().max().reshape(1) if gv.numel() else gmax_dev.zero_())
-        h = torch.cat([gg_loc, gmax_dev]).cpu().numpy()
-        return (float(_allreduce_np(comm, h[:1], sharded=sharded)[0]),
-                float(_allreduce_np(comm, h[1:], op="max", sharded=sharded)[0]))
+        h = red.reduce(sums=[dot1(gv.view(1, -1), 1, [gv])], maxes=[absmax(gv)])
+        return float(h[0]), float(h[1])
 
     status, message = 1, "STOP: TOTAL NO. of ITERATIONS REACHED LIMIT"
     nit = 0
     from ..utils.hooks import StepHooks
     hooks = StepHooks(comm, what="L-BFGS iterate")  # MULTIGRAD_CHECK_EVERY / _METRICS
     gg, gmax = gstats(g)
+    host0 = getattr(comm, "host_collectives", 0) if comm is not None else 0
     if gmax <= gtol:
         status, message = 0, "CONVERGENCE: NORM_OF_PROJECTED_GRADIENT_<=_PGTOL"
     else:
@@ -175,17 +172,15 @@ def _lbfgs_minimize_impl(obj, maxiter: int = 100, m: int = 10, ftol: float = 1e7
                 nonlocal nfev
                 torch.add(x, d, alpha=float(alpha), out=xt)
                 if dev_call is not None:
-                    # loss and the local d.g in ONE device->host copy
+                    # the loss (already global) and the local d.g: one reduction, one copy
                     lt, ga = dev_call(xt)
                     ga = ga.clone()
-                    pair = torch.cat([lt.reshape(1).double(), dot1(ga.view(1, -1), 1, [d]).reshape(1)])
-                    fa, da_loc = pair.cpu().numpy()
-                    fa = float(fa)
-                    da = float(_allreduce_np(comm, np.array([da_loc]), sharded=sharded)[0])
+                    h = red.reduce(sums=[dot1(ga.view(1, -1), 1, [d])], local=[lt.reshape(1)])
+                    da, fa = float(h[0]), float(h[1])
                 else:
                     fa, ga = obj(xt)
                     ga = ga.clone()
-                    da = gdot(ga, d)
+                    da = float(red.reduce(sums=[dot1(ga.view(1, -1), 1, [d])])[0])
                 nfev += 1
                 cache[alpha] = (fa, ga, da)
                 return fa, da
@@ -221,10 +216,9 @@ def _lbfgs_minimize_impl(obj, maxiter: int = 100, m: int = 10, ftol: float = 1e7
             g_row.copy_(g_new)
             nit = k + 1
             dv = dot(HX, 2 * m + 3, [s_vec, y_vec, g_row])  # (2m+3, 3)
-            gmax_dev.copy_(g_new.abs().max().reshape(1) if g_new.numel() else gmax_dev.zero_())
-            host = torch.cat([dv.reshape(-1), gmax_dev]).cpu().numpy()
-            dots = _allreduce_np(comm, host[:-1], sharded=sharded).reshape(2 * m + 3, 3)
-            gmax = float(_allreduce_np(comm, host[-1:], op="max", sharded=sharded)[0])
+            host = red.reduce(sums=[dv], maxes=[absmax(g_new)])
+            dots = host[:-1].reshape(2 * m + 3, 3)
+            gmax = float(host[-1])
             sy_new, yy_new = float(dots[2 * m, 1]), float(dots[2 * m + 1, 1])
             gg = float(dots[2 * m + 2, 2])
             inserted = sy_new > _EPS * yy_new and yy_new > 0
@@ -248,7 +242,10 @@ def _lbfgs_minimize_impl(obj, maxiter: int = 100, m: int = 10, ftol: float = 1e7
                 Yg[q] = dots[2 * m + 1, 2]
             f_old, f, g = f, f_new, g_new
             if callback is not None:
+                h0 = getattr(comm, "host_collectives", 0) if comm is not None else 0
                 callback(obj.full(x))
+                if comm is not None:  # the callback's own collectives are not the loop's
+                    host0 += getattr(comm, "host_collectives", 0) - h0
             if hooks.active:
                 hooks(k, f, None, (lambda: x) if not sharded else None)
             if gmax <= gtol:
@@ -257,12 +254,15 @@ def _lbfgs_minimize_impl(obj, maxiter: int = 100, m: int = 10, ftol: float = 1e7
             if (f_old - f) <= ftol * max(abs(f_old), abs(f), 1.0):
                 status, message = 0, "CONVERGENCE: REL_REDUCTION_OF_F_<=_FACTR*EPSMCH"
                 break
+    host_calls = (getattr(comm, "host_collectives", 0) - host0) if comm is not None else 0
+    red.check("L-BFGS")
     xf = obj.full(x)
     if getattr(obj, "finalize", None) is not None:
         xf = obj.finalize(x)
     return scipy.optimize.OptimizeResult(
         x=xf, fun=f, jac=g, nit=nit, nfev=nfev, njev=nfev, status=status,
-        success=status == 0, message=message)
+        success=status == 0, message=message, host_collectives=host_calls,
+        reduction=red.describe())
 
 
 def compact_coefficients(SY, YY, Sg, Yg, order):

@@ -41,11 +41,13 @@ import scipy.optimize
 import torch
 
 from ..ops.lbfgs import MultiDot, lincomb_
-from .lbfgs import _allreduce_np, _zoom
+from ._reduce import DeviceReducer
+from .lbfgs import _zoom
 
 __all__ = ["lbfgsb_minimize", "run_lbfgsb_device", "BoxObjective"]
 
 _EPS = np.finfo(np.float64).eps
+_B_CAP_MULTI = 1 << 16  # breakpoints per rank and Cauchy-point batch on several ranks
 
 
 class BoxObjective:
@@ -179,14 +181,20 @@ def _lbfgsb_minimize_impl(obj, lo=None, hi=None, maxiter: int = 100, m: int = 10
     status, message, nit = 1, "STOP: TOTAL NO. of ITERATIONS REACHED LIMIT", 0
     xt = torch.empty_like(x)
 
-    def allsum(a):
-        return _allreduce_np(comm, np.asarray(a, dtype=np.float64), sharded=sharded)
-
-    def allmax(a):
-        return _allreduce_np(comm, np.asarray(a, dtype=np.float64), op="max", sharded=sharded)
+    red = DeviceReducer(comm, sharded, dev)  # collective (may connect peer memory)
+    # the Cauchy-point batches all-gather at most (1 + B) x (2 + 2m) fp64 records per rank
+    red.reserve_gather((1 + (int(K) if K is not None else _B_CAP_MULTI)) * (2 + 2 * m) * 8)
 
     from ..utils.hooks import StepHooks
     hooks = StepHooks(comm, what="L-BFGS-B iterate")  # MULTIGRAD_CHECK_EVERY / _METRICS
+    host0 = getattr(comm, "host_collectives", 0) if comm is not None else 0
+
+    def run_callback(xv):
+        nonlocal host0
+        h0 = getattr(comm, "host_collectives", 0) if comm is not None else 0
+        callback(obj.full(xv))
+        if comm is not None:  # the callback's own collectives are not the loop's
+            host0 += getattr(comm, "host_collectives", 0) - h0
 
     for k in range(maxiter + 1):
         # ------------------------------------------------ copy A: pair dots + GCP inputs
@@ -200,22 +208,20 @@ def _lbfgsb_minimize_impl(obj, lo=None, hi=None, maxiter: int = 100, m: int = 10
         vecs = [d] if pending is None else [H.s(pending), H.y(pending), d]
         dots_dev = dot(H.HS, 2 * R, vecs)
         tc = torch.where(free_path & torch.isfinite(t), t, torch.full_like(t, math.inf))
-        scal = torch.stack([(d.double() * d.double()).sum(),
-                            pg.max().double() if n else torch.zeros((), dtype=torch.float64,
-                                                                    device=dev),
-                            torch.isfinite(tc).sum().double()])
-        packA = torch.cat([scal, dots_dev.reshape(-1)]).cpu().numpy()
-        dd_l, pg_l, nfin_l = packA[:3]
-        dots_l = packA[3:].reshape(2 * R, len(vecs))
-        red = allsum(np.concatenate([[dd_l], dots_l.reshape(-1)]))
-        dd, dots_np = red[0], red[1:].reshape(2 * R, len(vecs))
-        pgmax = float(allmax([pg_l])[0])
+        pg_l = pg.max().double() if n else torch.zeros((), dtype=torch.float64, device=dev)
+        # one reduction and one copy: [d.d, HS.vecs (summed), max|pg| (max), #finite (local)]
+        packA = red.reduce(sums=[(d.double() * d.double()).sum(), dots_dev],
+                           maxes=[pg_l], local=[torch.isfinite(tc).sum()])
+        dd = packA[0]
+        dots_np = packA[1:1 + 2 * R * len(vecs)].reshape(2 * R, len(vecs))
+        pgmax = float(packA[-2])
+        nfin_l = packA[-1]
         if pending is not None:
             H.accept(pending, dots_np[:, :2])
             pending = None
         Wd = dots_np[:, -1]  # HS rows . d
         if k > 0 and callback is not None:
-            callback(obj.full(x))
+            run_callback(x)
         if pgmax <= pgtol:
             status, message = 0, "CONVERGENCE: NORM_OF_PROJECTED_GRADIENT_<=_PGTOL"
             break
@@ -226,7 +232,7 @@ def _lbfgsb_minimize_impl(obj, lo=None, hi=None, maxiter: int = 100, m: int = 10
         rows, fac = H.rows(idx)
         th = H.theta
         tstar, cvec = _cauchy_point(dd, Wd[rows] * fac, M, th, tc, int(nfin_l), g, H.HS,
-                                    rows, fac, comm if sharded else None, K)
+                                    rows, fac, red, K)
         xcp = torch.minimum(torch.maximum(x - tstar * g, lo), hi)
         free = (xcp > lo) & (xcp < hi)
         # ------------------------------------------------ copy B: subspace inner products
@@ -248,8 +254,7 @@ def _lbfgsb_minimize_impl(obj, lo=None, hi=None, maxiter: int = 100, m: int = 10
             GA = _gram(H.HS[rows_d[:, None], act[None, :]].double())
         else:
             GA = torch.zeros((0, 0), dtype=torch.float64, device=dev)
-        packB = torch.cat([WtZr.reshape(-1), GA.reshape(-1)]).cpu().numpy()
-        redB = allsum(packB)
+        redB = red.reduce(sums=[WtZr, GA])
         WtZr_np = redB[:2 * R]
         GA_np = redB[2 * R:].reshape(kk2 * 2, kk2 * 2) if kk2 else np.zeros((0, 0))
         if kk2:
@@ -271,7 +276,7 @@ def _lbfgsb_minimize_impl(obj, lo=None, hi=None, maxiter: int = 100, m: int = 10
         # ------------------------------------------------ line search along x + a dirn
         a1 = 1.0
         if k == 0 or not H.order:
-            dnorm2 = float(allsum([(dirn.double() ** 2).sum().item()])[0])
+            dnorm2 = float(red.reduce(sums=[(dirn.double() ** 2).sum()])[0])
             a1 = min(1.0, 1.0 / math.sqrt(max(dnorm2, 1e-300)))
         cache = {}
         d0_box = [None]
@@ -282,19 +287,16 @@ def _lbfgsb_minimize_impl(obj, lo=None, hi=None, maxiter: int = 100, m: int = 10
             if dev_call is not None:
                 lt, ga = dev_call(xt)
                 ga = ga.clone()
-                parts = [lt.reshape(1).double(), (ga.double() * dirn.double()).sum().reshape(1)]
-                if d0_box[0] is None:
-                    parts.append((g.double() * dirn.double()).sum().reshape(1))
-                vals = torch.cat(parts).cpu().numpy()
-                fa = float(vals[0])
-                red2 = allsum(vals[1:])
             else:
-                fa, ga = obj(xt)
+                fl, ga = obj(xt)
                 ga = ga.clone()
-                parts = [(ga.double() * dirn.double()).sum().item()]
-                if d0_box[0] is None:
-                    parts.append((g.double() * dirn.double()).sum().item())
-                red2 = allsum(parts)
+                lt = torch.tensor([fl], dtype=torch.float64)
+            # directional derivative(s) summed over the ranks with the (global) loss: one copy
+            parts = [(ga.double() * dirn.double()).sum()]
+            if d0_box[0] is None:
+                parts.append((g.double() * dirn.double()).sum())
+            red2 = red.reduce(sums=parts, local=[lt.reshape(1)])
+            fa = float(red2[-1])
             if d0_box[0] is None:
                 d0_box[0] = float(red2[1])
             nfev += 1
@@ -306,8 +308,9 @@ def _lbfgsb_minimize_impl(obj, lo=None, hi=None, maxiter: int = 100, m: int = 10
             # the projected subspace step is not a descent direction: truncate instead
             ratio = torch.where(du > 0, (hi - xcp) / du, torch.where(du < 0, (lo - xcp) / du,
                                                                     torch.full_like(du, math.inf)))
-            rmin_l = float(ratio.min().item()) if ratio.numel() else math.inf
-            rmin = -float(allmax([-rmin_l])[0])
+            rmin_l = -ratio.min().double() if ratio.numel() else \
+                torch.full((), -math.inf, dtype=torch.float64, device=dev)
+            rmin = -float(red.reduce(maxes=[rmin_l])[0])
             dirn = xcp + min(1.0, rmin) * du - x
             cache.clear()
             d0_box[0] = None
@@ -332,17 +335,20 @@ def _lbfgsb_minimize_impl(obj, lo=None, hi=None, maxiter: int = 100, m: int = 10
         if (f_old - f) <= ftol * max(abs(f_old), abs(f), 1.0):
             status, message = 0, "CONVERGENCE: REL_REDUCTION_OF_F_<=_FACTR*EPSMCH"
             if callback is not None:
-                callback(obj.full(x))
+                run_callback(x)
             break
+    host_calls = (getattr(comm, "host_collectives", 0) - host0) if comm is not None else 0
+    red.check("L-BFGS-B")
     xf = obj.full(x)
     if getattr(obj, "finalize", None) is not None:
         xf = obj.finalize(x)
     return scipy.optimize.OptimizeResult(
         x=xf, fun=f, jac=g, nit=nit, nfev=nfev, njev=nfev, status=status,
-        success=status == 0, message=message)
+        success=status == 0, message=message, host_collectives=host_calls,
+        reduction=red.describe())
 
 
-def _cauchy_point(dd, p0, M, theta, tc, nfin, g, HS, rows, fac, comm, K):
+def _cauchy_point(dd, p0, M, theta, tc, nfin, g, HS, rows, fac, red, K):
     """Generalized Cauchy point ``t*`` and ``c = W'(x^cp - x)`` (Byrd et al. 1995,
     algorithm CP), over the breakpoints in increasing order, in batches.
 
@@ -361,11 +367,12 @@ def _cauchy_point(dd, p0, M, theta, tc, nfin, g, HS, rows, fac, comm, K):
     order = torch.argsort(tc)
     rows_t = torch.as_tensor(rows, dtype=torch.int64, device=dev)
     fac_t = torch.as_tensor(fac, dtype=torch.float64, device=dev)
+    comm = None if red is None else red.comm
     multi = comm is not None and comm.size > 1
     # batch sizes: K if given, else geometric from 2^14 (the Cauchy point usually lies among
     # the first few thousand breakpoints, and a scan costs O(2k x batch) in fp64) up to
     # 2^16 per rank (several ranks: one all-gather per batch) or 2^20 (one rank)
-    B_cap = int(K) if K is not None else (1 << 16 if multi else 1 << 20)
+    B_cap = int(K) if K is not None else (_B_CAP_MULTI if multi else 1 << 20)
     B = int(K) if K is not None else min(1 << 14, B_cap)
     ptr = 0
     while True:
@@ -382,13 +389,14 @@ def _cauchy_point(dd, p0, M, theta, tc, nfin, g, HS, rows, fac, comm, K):
             rec[nb:, 1:] = 0.0
             hdr = torch.tensor([[float(left)] + [0.0] * (1 + k2)], dtype=torch.float64, device=dev)
             mine = torch.cat([hdr, rec]).contiguous()
-            allr = torch.empty((comm.size,) + tuple(mine.shape), dtype=torch.float64, device=dev)
-            comm.all_gather_into_tensor(allr.reshape(-1), mine.reshape(-1))
-            lefts = allr[:, 0, 0].cpu().numpy()
+            allr = red.all_gather(mine)   # peer memory / RCCL: [W, 1 + B, 2 + k2]
+            # one copy: every rank's count of unscanned breakpoints and its B-th breakpoint
+            hdr = torch.stack([allr[:, 0, 0], allr[:, B, 0]], 1).cpu().numpy()
+            lefts = hdr[:, 0]
             t_cut = math.inf
             for r in range(comm.size):
                 if lefts[r] > B:
-                    t_cut = min(t_cut, float(allr[r, 1 + B - 1, 0]))
+                    t_cut = min(t_cut, float(hdr[r, 1]))
             recs = allr[:, 1:].reshape(-1, 2 + k2)
             keep = recs[:, 0] <= t_cut
             recs = recs[keep & torch.isfinite(recs[:, 0])]

@@ -111,6 +111,7 @@ class Comm:
     name: str = "WORLD"
     uid: str = "w"
     global_ranks: Sequence[int] = (0,)
+    host_collectives: int = 0   # collectives run on the host (TorchComm counts them)
 
     # ------------------------------------------------------------------ mpi4py-style
     def Get_rank(self) -> int:
@@ -298,6 +299,10 @@ class TorchComm(Comm):
         self.uid = uid
         self.global_ranks = tuple(int(r) for r in global_ranks)
         self._nsplit = 0
+        # collectives that ran on the host (gloo: CPU tensors, device tensors staged through
+        # host memory, object collectives) -- the optimizers' hot loops are checked to make
+        # none (device L-BFGS: zero per iteration on GPUs)
+        self.host_collectives = 0
         self._cpu = cpu_backend
         self._dev = dev_backend
         if use_device is None:
@@ -318,6 +323,10 @@ class TorchComm(Comm):
                 c10d.PrefixStore(f"mg/{self.uid}/rccl", self.store), self.rank, self.size, opts)
         return self._dev
 
+    def device_collectives(self) -> bool:
+        """Whether device tensors are reduced on the devices (RCCL), not staged via gloo."""
+        return self._use_device and self._device_backend() is not None
+
     def _backend_for(self, tensor: torch.Tensor):
         if tensor.device.type == "cpu":
             return self._cpu, False
@@ -328,6 +337,8 @@ class TorchComm(Comm):
 
     def _run(self, fn, tensor: torch.Tensor, async_op: bool):
         backend, staged = self._backend_for(tensor)
+        if backend is self._cpu:
+            self.host_collectives += 1
         if staged:
             host = tensor.detach().cpu()
             fn(backend, host).wait()
@@ -388,6 +399,7 @@ class TorchComm(Comm):
                 return work
             work.wait()
             return None
+        self.host_collectives += 1
         src = tensor.detach().reshape(-1).cpu()
         outs = [torch.empty_like(src) for _ in range(self.size)]
         self._cpu.allgather([outs], [src]).wait()
@@ -413,10 +425,12 @@ class TorchComm(Comm):
 
     # ------------------------------------------------------------------ objects
     def barrier(self) -> None:
+        self.host_collectives += 1
         self._cpu.barrier().wait()
 
     def _bcast_bytes(self, data: Optional[bytes], root: int) -> bytes:
         c10d = _c10d()
+        self.host_collectives += 1
         n = torch.tensor([len(data) if self.rank == root else 0], dtype=torch.int64)
         opts = c10d.BroadcastOptions()
         opts.rootRank = int(root)
@@ -437,6 +451,7 @@ class TorchComm(Comm):
         return obj if self.rank == root else pickle.loads(out)
 
     def allgather(self, obj):
+        self.host_collectives += 1
         data = pickle.dumps(obj, protocol=pickle.HIGHEST_PROTOCOL)
         n = torch.tensor([len(data)], dtype=torch.int64)
         ns = [torch.empty(1, dtype=torch.int64) for _ in range(self.size)]

@@ -35,10 +35,13 @@ import torch
 
 __all__ = ["OneShotAllReduce", "CollectiveTimeout", "oneshot_enabled", "oneshot_mode",
            "connect", "get_oneshot", "maybe_oneshot", "MAX_FLOATS", "MAX_RANKS", "TwoShot",
+           "WideOneShot", "get_wide_oneshot", "MAX_WIDE",
            "connect_twoshot", "twoshot_enabled", "get_twoshot_allreduce", "acquire_twoshot",
-           "release_twoshot", "release_twoshot_allreduce", "status", "STRESS_REPS"]
+           "release_twoshot", "release_twoshot_allreduce", "status", "STRESS_REPS",
+           "peer_all_gather"]
 
 MAX_FLOATS = 64
+MAX_WIDE = 1024    # fp64 values per wide one-shot call (csrc/xgmi.h kXwMax)
 MAX_RANKS = 8
 STRESS_REPS = 32   # back-to-back device-only exchanges in each connect-time self-test
 
@@ -136,13 +139,17 @@ class OneShotAllReduce:
                 f"skipped a collective or fell behind by more than MULTIGRAD_ONESHOT_TIMEOUT; "
                 f"call reset() on every rank (collective) before reusing the communicator")
 
+    @staticmethod
+    def region_bytes() -> int:
+        return 0  # the extension's default: the one-shot region
+
     def reset(self, comm) -> None:
         """Collective: return the protocol to its initial state on every rank (after a
         timeout was handled).  Every rank's kernels are drained first."""
         from ..ops._ext import ext
         torch.cuda.synchronize()
         comm.barrier()
-        ext().xgmi_zero(self.base)
+        ext().xgmi_zero(self.base, self.region_bytes())
         self.seq.zero_()
         self.err.zero_()
         torch.cuda.synchronize()
@@ -189,17 +196,20 @@ class OneShotAllReduce:
         self.peers, self.base = [], 0
 
 
-def connect(comm, timeout_s: float = 5.0, test: bool = True) -> Optional[OneShotAllReduce]:
+def connect(comm, timeout_s: float = 5.0, test: bool = True,
+            cls=None) -> Optional[OneShotAllReduce]:
     """Collective: export, exchange and map the regions of every rank of ``comm``, then
     self-test.  Each phase ends with an all-gather of the per-rank verdicts, so all ranks
     take the same branch; returns None (use RCCL) if any rank failed any phase -- a
-    missing native extension included."""
+    missing native extension included.  ``cls``: :class:`OneShotAllReduce` (default) or
+    :class:`WideOneShot`."""
+    cls = OneShotAllReduce if cls is None else cls
     E = None
     base, handle = 0, None
     try:
         from ..ops._ext import ext
         E = ext()
-        base = E.xgmi_alloc()
+        base = E.xgmi_alloc(cls.region_bytes())
         handle = bytes(E.xgmi_handle(base))
     except Exception as exc:  # noqa: BLE001  (no extension / no IPC on this rank)
         _debug(exc)
@@ -218,22 +228,52 @@ def connect(comm, timeout_s: float = 5.0, test: bool = True) -> Optional[OneShot
                     E.xgmi_close(p)
             if base:
                 E.xgmi_free(base)
-        _record(comm, "one-shot", ok=False, stress_exchanges=0,
+        _record(comm, cls.kind, ok=False, stress_exchanges=0,
                 fallback="RCCL: peer-memory export/map unavailable on some rank")
         return None
-    ar = OneShotAllReduce(comm.rank, comm.size, base, peers, timeout_s)
+    ar = cls(comm.rank, comm.size, base, peers, timeout_s)
     comm.barrier()  # every region is zeroed and mapped before any rank writes into it
     ok = ar.self_test() if test else True
     verdicts = comm.allgather(bool(ok))
     if not all(verdicts):
         torch.cuda.synchronize()
         ar.close()
-        _record(comm, "one-shot", ok=False, stress_exchanges=0,
+        _record(comm, cls.kind, ok=False, stress_exchanges=0,
                 fallback=f"RCCL: stress self-test failed on rank(s) "
                          f"{[r for r, v in enumerate(verdicts) if not v]}")
         return None
-    _record(comm, "one-shot", ok=True, stress_exchanges=STRESS_REPS if test else 0, fallback=None)
+    _record(comm, cls.kind, ok=True, stress_exchanges=STRESS_REPS if test else 0, fallback=None)
     return ar
+
+
+def device_share(comm) -> int:
+    """How many ranks of ``comm`` (this one included) run on this rank's GPU (collective on
+    first use, cached): 1 on a normal one-process-per-GPU node, W when W processes share one
+    GPU (the single-GPU rehearsals of multi-rank runs)."""
+    n = getattr(comm, "_device_share", None)
+    if n is None:
+        import socket
+        ident = None
+        try:
+            from ..ops._ext import ext
+            ident = (socket.gethostname(), str(ext().device_pci_bus_id()))
+        except Exception as exc:  # noqa: BLE001
+            _debug(exc)
+        ids = comm.allgather(ident)
+        n = max(1, sum(1 for i in ids if i is not None and i == ident))
+        try:
+            comm._device_share = n
+        except AttributeError:
+            pass
+    return int(n)
+
+
+# Workgroups of one two-shot exchange launch with the GPU to itself (the grid-stride loop
+# covers any size).  Exchange workgroups wait for their peers' flags; when several ranks
+# share one GPU, every rank's grid is cut to 1/share of this so all of them can be resident
+# together and no waiting grid can keep a peer's signalling workgroup off the GPU (an
+# exchange grid that fills the GPU made the 4- and 8-process one-GPU rehearsals time out).
+TWOSHOT_GRID = 1024
 
 
 def _debug(exc) -> None:
@@ -272,6 +312,80 @@ def get_oneshot(comm) -> Optional[OneShotAllReduce]:
     return ar or None
 
 
+class WideOneShot(OneShotAllReduce):
+    """fp64 one-shot all-reduce of up to :data:`MAX_WIDE` values per call, a summed part
+    followed by a max-reduced part, both in rank order (every rank gets the same bits):
+    the optimizers' per-iteration reductions (device L-BFGS / L-BFGS-B inner products,
+    line-search directional derivatives, max|g|), stream ordered, no host round trip.
+    Build it with :func:`get_wide_oneshot` (collective, self-tested)."""
+
+    kind = "wide one-shot"
+
+    @staticmethod
+    def region_bytes() -> int:
+        from ..ops._ext import ext
+        return int(ext().xgmi_wide_region_bytes())
+
+    @staticmethod
+    def supports(t: torch.Tensor, op=None) -> bool:
+        return (t.is_cuda and t.dtype == torch.float64 and t.is_contiguous()
+                and 1 <= t.numel() <= MAX_WIDE)
+
+    def __call__(self, t: torch.Tensor, nsum: Optional[int] = None, nmax: int = 0) -> torch.Tensor:
+        """In place: ``t[:nsum]`` summed, ``t[nsum:nsum + nmax]`` max-reduced across the
+        ranks (``nsum`` defaults to the rest of ``t``)."""
+        from ..ops._ext import ext
+        nsum = t.numel() - nmax if nsum is None else int(nsum)
+        ext().xgmi_allreduce_wide(t, int(nsum), int(nmax), self.peers, self.rank, self.seq,
+                                  self.err, self.timeout_s)
+        return t
+
+    def self_test(self, reps: int = STRESS_REPS) -> bool:
+        """``reps`` back-to-back exchanges without host synchronisation, each with
+        rank- and call-dependent values whose sums and maxima are exact in fp64 (about 47
+        significant bits: integers up to ~2^23 with 2^-24 fractions), sizes up to
+        the full width; verified once at the end (the test hook
+        ``MULTIGRAD_XGMI_SELFTEST_CORRUPT`` perturbs one rank's contribution)."""
+        dev = self.seq.device
+        corrupt = _corrupt_rank() == self.rank
+        W = self.size
+        sizes = [1 + (131 * i) % MAX_WIDE for i in range(reps)]
+        sizes[-1] = MAX_WIDE
+        bufs, outs = [], []
+        for i, n in enumerate(sizes):
+            nmax = min(n // 3, 16)
+            t = torch.arange(n, dtype=torch.float64, device=dev) * 2.0 ** -24
+            t += (self.rank + 1) * (i + 1) * 1024.0
+            if corrupt and i == reps // 2:
+                t[0] += 0.5
+            self(t, n - nmax, nmax)
+            bufs.append((n, nmax))
+            outs.append(t)
+        got = [o.cpu() for o in outs]
+        for i, ((n, nmax), g) in enumerate(zip(bufs, got)):
+            base = torch.arange(n, dtype=torch.float64) * 2.0 ** -24
+            want = base * W + (i + 1) * 1024.0 * W * (W + 1) / 2
+            want[n - nmax:] = base[n - nmax:] + W * (i + 1) * 1024.0
+            if not torch.equal(g, want):
+                return False
+        return self.ok()
+
+
+def get_wide_oneshot(comm) -> Optional[WideOneShot]:
+    """The communicator's wide one-shot context, connecting it now if needed (collective:
+    call on every rank); None when disabled (``MULTIGRAD_ALLREDUCE=rccl``), on CPU, on more
+    than :data:`MAX_RANKS` ranks or when peer memory is unavailable (the caller uses RCCL
+    or gloo)."""
+    if comm is None or comm.size == 1 or not oneshot_enabled() or comm.size > MAX_RANKS:
+        return None
+    if not torch.cuda.is_available():
+        return None
+    ar = getattr(comm, "_wide_oneshot", None)
+    if ar is None:
+        ar = comm._wide_oneshot = connect(comm, _timeout_s(), cls=WideOneShot) or False
+    return ar or None
+
+
 # ============================================================================ two-shot
 def twoshot_enabled() -> bool:
     """Whether the ZeRO engine may sum its dense gradient with the two-shot kernel
@@ -295,10 +409,12 @@ class TwoShot:
 
     kind = "two-shot"
 
-    def __init__(self, comm, numel: int, regions, peers, timeout_s: float):
+    def __init__(self, comm, numel: int, regions, peers, timeout_s: float, share: int = 1):
         from ..ops._ext import ext
         E = ext()
         self.rank, self.size = comm.rank, comm.size
+        # grid cap of every launch (TWOSHOT_GRID / ranks sharing this GPU)
+        self.block_cap = max(16, TWOSHOT_GRID // max(1, int(share)))
         self.numel = int(numel)
         self.regions = regions            # (grad, theta, flags) base addresses, this rank
         self.gpeers, self.tpeers, self.fpeers = peers
@@ -315,6 +431,10 @@ class TwoShot:
         self.holders = 0
         self.pinned = False
 
+    def _blocks(self, max_blocks: int) -> int:
+        mb = int(max_blocks)
+        return self.block_cap if mb <= 0 else min(mb, self.block_cap)
+
     def slice(self, rank: Optional[int] = None):
         """Owned float range ``(lo, n)`` of ``rank`` (default: this rank)."""
         r = self.rank if rank is None else rank
@@ -326,8 +446,9 @@ class TwoShot:
              host_step: Optional[int] = None, lr: float = 0.0, b1: float = 0.9, b2: float = 0.999,
              eps: float = 1e-8, max_blocks: int = 0) -> None:
         """Enqueue one exchange on the current stream.  ``mode`` 0: theta = sum of the
-        gradients (self-test); 1: unbounded Adam; 2/3: bounded (3: legacy Jacobian).
-        ``max_blocks`` caps the grid (0: the default 1024)."""
+        gradients (self-test); 1: unbounded Adam; 2/3: bounded (3: legacy Jacobian);
+        4: reduce-scatter into ``u``; 5: all-gather of ``u`` (:meth:`reduce_scatter_`,
+        :meth:`all_gather_`).  ``max_blocks`` caps the grid (0: the default 1024)."""
         from ..ops._ext import ext
         if not self.regions:
             raise RuntimeError("two-shot context used after close() (its peer memory is "
@@ -340,7 +461,7 @@ class TwoShot:
                            self._step0 if step is None else step, self.seq, self.err,
                            [float(-1 if host_step is None else host_step), float(lr), float(b1),
                             float(b2), float(eps), self.timeout_s, float(traj_stride),
-                            float(max_blocks)])
+                            float(self._blocks(max_blocks))])
 
     def pack(self, lo: int, n: int, mode: int, m=None, v=None, traj=None, traj_stride: int = 0,
              step: Optional[torch.Tensor] = None, host_step: Optional[int] = None,
@@ -358,10 +479,20 @@ class TwoShot:
             int(mode), None, m, v, None, None, None, traj,
             self._step0 if step is None else step, self.seq, self.err,
             [float(-1 if host_step is None else host_step), float(lr), float(b1), float(b2),
-             float(eps), self.timeout_s, float(traj_stride), float(max_blocks)])
+             float(eps), self.timeout_s, float(traj_stride), float(self._blocks(max_blocks))])
 
     def check(self, where: str = "", comm=None) -> None:
         OneShotAllReduce.check(self, where, comm)  # same err/seq protocol words
+
+    def reduce_scatter_(self, out: torch.Tensor, lo: int, n: int, max_blocks: int = 0) -> None:
+        """Mode 4: ``out[:n]`` = rank-order sum over the ranks of ``grad[lo:lo+n]`` (this
+        rank's owned slice of every peer's gradient region); nothing is pushed."""
+        self.step(lo, n, 4, u=out, max_blocks=max_blocks)
+
+    def all_gather_(self, src: torch.Tensor, lo: int, n: int, max_blocks: int = 0) -> None:
+        """Mode 5: ``theta[lo:lo+n]`` = ``src[:n]`` on every rank (this rank's slice pushed
+        into every peer's parameter region); nothing is pulled."""
+        self.step(lo, n, 5, u=src, max_blocks=max_blocks)
 
     def all_reduce_(self, t: torch.Tensor) -> torch.Tensor:
         """In-place sum of a contiguous fp32 tensor of at most ``numel`` elements over the
@@ -502,6 +633,36 @@ def get_twoshot_allreduce(comm, numel: int, hold: bool = False) -> Optional[TwoS
     return ts or None
 
 
+def peer_all_gather(comm, out: torch.Tensor, inp: torch.Tensor) -> bool:
+    """``out`` (``[W * inp.numel()]`` elements, any dtype) = every rank's ``inp`` in rank
+    order, through a cached two-shot context (mode 5: each rank pushes its piece into every
+    peer's region; the bits are moved, never added, so fp64 and integer data pass
+    unchanged).  Collective.  False (nothing done) where peer memory is unavailable; the
+    caller then uses ``comm.all_gather_into_tensor``."""
+    if comm is None or comm.size < 2 or not inp.is_cuda:
+        return False
+    nb = inp.numel() * inp.element_size()
+    if nb % 4 or not inp.is_contiguous() or not out.is_contiguous():
+        return False
+    n = -(-(nb // 4) // 4) * 4  # floats per rank, float4 aligned
+    ts = get_twoshot_allreduce(comm, n * comm.size, hold=True)
+    if ts is None:
+        return False
+    try:
+        src = inp.reshape(-1).view(torch.float32)
+        if src.numel() != n or src.data_ptr() % 16:
+            pad = torch.zeros(n, dtype=torch.float32, device=inp.device)
+            pad[:src.numel()] = src
+            src = pad
+        ts.all_gather_(src, comm.rank * n, n)
+        k = nb // 4
+        rows = ts.theta[:n * comm.size].view(comm.size, n)[:, :k]
+        out.reshape(-1).view(torch.float32).view(comm.size, k).copy_(rows)
+    finally:
+        release_twoshot_allreduce(ts)
+    return True
+
+
 def release_twoshot_allreduce(ts: Optional[TwoShot]) -> None:
     """Give back a context taken with ``get_twoshot_allreduce(..., hold=True)``."""
     if ts:
@@ -580,7 +741,7 @@ def connect_twoshot(comm, numel: int, timeout_s: Optional[float] = None,
         _record(comm, "two-shot", ok=False, numel=numel, stress_exchanges=0,
                 fallback="RCCL: peer-memory export/map unavailable on some rank")
         return None
-    ts = TwoShot(comm, numel, tuple(regions), peers, timeout_s)
+    ts = TwoShot(comm, numel, tuple(regions), peers, timeout_s, share=device_share(comm))
     comm.barrier()
     ok = ts.self_test() if test else True
     verdicts = comm.allgather(bool(ok))
@@ -590,6 +751,6 @@ def connect_twoshot(comm, numel: int, timeout_s: Optional[float] = None,
                 fallback=f"RCCL: stress self-test failed on rank(s) "
                          f"{[r for r, v in enumerate(verdicts) if not v]}")
         return None
-    _record(comm, "two-shot", ok=True, numel=numel,
+    _record(comm, "two-shot", ok=True, numel=numel, grid=ts.block_cap,
             stress_exchanges=STRESS_REPS if test else 0, fallback=None)
     return ts
