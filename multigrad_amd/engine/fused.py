@@ -181,6 +181,9 @@ class FusedAdamEngine:
         # between consecutive graph launches are paid once per block, not per step
         # (profiles/graph_modes/); MULTIGRAD_GRAPH_STEPS, 1 = one step per graph
         self.graph_steps = max(1, int(os.environ.get("MULTIGRAD_GRAPH_STEPS", "16")))
+        # direct step() calls replay graphs only on request (engine/generic.py step())
+        from .generic import _step_replay_default
+        self.step_replay = _step_replay_default()
         self._kgraph = None
         self.graph = None
         self._capturing = False
@@ -1095,8 +1098,9 @@ class FusedAdamEngine:
     def _hstep(self, idx: Optional[int] = None):
         """The 0-based step for eager launches; None inside a graph capture and for every
         launch of a graph-mode engine (the Adam kernels then keep the step in device
-        memory, so graph replays and eager launches agree)."""
-        if self._capturing or ((self.use_graph or self.device_step) and self.pipeline):
+        memory, so graph replays and eager launches -- e.g. direct step() calls, which
+        launch eagerly -- agree)."""
+        if self._capturing or self.use_graph or (self.device_step and self.pipeline):
             return None
         return self.step_host if idx is None else idx
 
@@ -1161,14 +1165,14 @@ class FusedAdamEngine:
             return
         if not self._block_ok():
             for _ in range(n):
-                self.step()
+                self._step(replay=True)
             return
         if self.step_host + n > self.nsteps and self.history.mode == "full":
             raise RuntimeError("more steps than the trajectory buffer was sized for")
         self._run_steps(n)
 
-    def _raw_step(self):
-        if self.use_graph and (self.pending or not self.pipeline):
+    def _raw_step(self, replay: bool = True):
+        if replay and self.use_graph and (self.pending or not self.pipeline):
             if self.graph is None:
                 self._capture()
             self.graph.replay()
@@ -1180,11 +1184,17 @@ class FusedAdamEngine:
 
     @on_engine_stream
     def step(self):
-        """Enqueue one optimizer step (asynchronous on GPU)."""
+        """Enqueue one optimizer step (asynchronous on GPU).  A direct call launches eagerly
+        even in graph mode unless ``step_replay`` is set (``MULTIGRAD_STEP_REPLAY=1``), as
+        :meth:`GraphAdamEngine.step <multigrad_amd.engine.generic.GraphAdamEngine.step>`;
+        :meth:`steps` and ``run_adam`` replay."""
+        self._step(replay=self.step_replay)
+
+    def _step(self, replay: bool = True):
         assert self.ready, "call setup() first"
         if self.step_host >= self.nsteps and self.history.mode == "full":
             raise RuntimeError("more steps than the trajectory buffer was sized for")
-        self._raw_step()
+        self._raw_step(replay)
         if self.history.mode != "full" and self.traj_loc is None:
             if self.pipeline:
                 st = self.history.stride

@@ -124,6 +124,11 @@ def _leaf_view(p: torch.Tensor, shape) -> torch.Tensor:
     return p.detach().view(shape).requires_grad_(True)
 
 
+def _step_replay_default() -> bool:
+    """``MULTIGRAD_STEP_REPLAY``: whether direct ``step()`` calls may replay graphs."""
+    return os.environ.get("MULTIGRAD_STEP_REPLAY", "0").strip().lower() in ("1", "on", "true", "yes")
+
+
 class GraphAdamEngine:
     """Adam over a generic :class:`~multigrad_amd.models.onepoint.OnePointModel` (or a
     :class:`~multigrad_amd.models.onepoint.OnePointGroup` of them).
@@ -147,6 +152,10 @@ class GraphAdamEngine:
         self.graph = None
         self._kgraph = None
         self.graph_steps = max(1, int(os.environ.get("MULTIGRAD_GRAPH_STEPS", "16")))
+        # direct step() calls replay graphs only when the caller promises to launch nothing
+        # on the legacy default stream between them (engine/_stream.py); the engine's own
+        # drivers (steps(), run_adam, run_simple_grad_descent) always may
+        self.step_replay = _step_replay_default()
         self.use_graph = False
         self.fallback_reason = None
         self.oneshot = None          # main-communicator one-shot (group loss)
@@ -632,7 +641,7 @@ class GraphAdamEngine:
                 if self.history.mode != "full" and self.traj_loc is None:
                     self.history.record(self.step_host - 1, self.p[:self.P])
             else:
-                self.step()
+                self._step()
                 n -= 1
 
     def _drive(self, nsteps: int, hooks, *hook_args, **hook_kw):
@@ -642,7 +651,7 @@ class GraphAdamEngine:
             self.steps(nsteps)
             return
         for i in range(int(nsteps)):
-            self.step()
+            self._step()
             hooks(i, self.loss, *hook_args, **hook_kw)
 
     _TUNE = 6       # steps per timed window of the auto policy
@@ -698,11 +707,28 @@ class GraphAdamEngine:
 
     @on_engine_stream
     def step(self):
+        """One optimizer step.  A direct call launches the step eagerly even in graph mode,
+        unless ``step_replay`` is set (``MULTIGRAD_STEP_REPLAY=1``): between direct calls
+        the caller may launch kernels on the legacy default stream and synchronise, after
+        which a graph replay computes garbage on this HIP runtime (docs/design.md "Graph
+        replays and the default stream"); a caller that keeps its own GPU work inside
+        :meth:`stream` may opt in.  The engine's drivers (:meth:`steps`, ``run_adam``,
+        ``run_simple_grad_descent``) own every launch and replay."""
+        self._step(replay=self.step_replay)
+
+    def _step(self, replay: bool = True):
         assert self.ready, "call setup() first"
         if self.step_host >= self.nsteps and (self.history.mode == "full" or self.traj_loc is not None
                                               or self.mode == "sgd"):
             raise RuntimeError("more steps than the trajectory buffer was sized for")
         key = self._step_key()
+        if not replay and self.use_graph:
+            self._body(self.step_host, key)
+            self._dev_step_stale = True
+            self.step_host += 1
+            if self.history.mode != "full" and self.traj_loc is None:
+                self.history.record(self.step_host - 1, self.p[:self.P])
+            return
         if self.use_graph and self.graph_req is None and self.tuning is None and \
                 self.nsteps > 3 * self._TUNE + self._TUNE_WARM:
             self._tuned_step(key)

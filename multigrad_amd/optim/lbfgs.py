@@ -107,25 +107,27 @@ def _lbfgs_minimize_impl(obj, maxiter: int = 100, m: int = 10, ftol: float = 1e7
     f, g = obj(x)
     g = g.clone()  # the objective may return a view of a buffer the next evaluation reuses
     nfev = 1
-    # rows 0..2m-1: the S and Y slots; 2m, 2m+1: the new pair s, y; 2m+2: the new gradient.
-    # One multi-dot of all rows against (s, y, g) gives every scalar an iteration needs
-    # (s.y, y.y, the new Gram rows, S^T g, Y^T g, g.g), and max|g| rides along in the same
-    # reduction and device->host copy: with the line search's one copy per evaluation, a
-    # typical iteration makes two.
-    HX = torch.zeros((2 * m + 3, n), dtype=torch.float32, device=dev)
-    HS = HX[:2 * m]
-    s_vec, y_vec, g_row = HX[2 * m], HX[2 * m + 1], HX[2 * m + 2]
-    dot = MultiDot(2 * m + 3, n, dev)
+    # A ring of R = m + 1 pair slots: rows 0..R-1 hold s, rows R..2R-1 hold y, row 2R the
+    # current gradient.  The new pair is written straight into the spare slot (no copy when
+    # it is accepted); one multi-dot of all rows against (s_new, y_new, g) gives every scalar
+    # an iteration needs (s.y, y.y, the new Gram rows, S^T g, Y^T g, g.g), and max|g| rides
+    # along in the same reduction and device->host copy: with the line search's one copy per
+    # evaluation, a typical iteration makes two.
+    R = m + 1
+    HX = torch.zeros((2 * R + 1, n), dtype=torch.float32, device=dev)
+    HS = HX[:2 * R]
+    g_row = HX[2 * R]
+    dot = MultiDot(2 * R + 1, n, dev)
     dot1 = MultiDot(1, n, dev)
-    SY = np.zeros((m, m))
-    YY = np.zeros((m, m))
-    Sg = np.zeros(m)
-    Yg = np.zeros(m)
-    order: list = []  # ring slots, oldest -> newest
+    SY = np.zeros((R, R))
+    YY = np.zeros((R, R))
+    Sg = np.zeros(R)
+    Yg = np.zeros(R)
+    order: list = []  # accepted slots, oldest -> newest (at most m)
     d = torch.empty_like(x)
     xt = torch.empty_like(x)
     dev_call = getattr(obj, "device_call", None) if dev.type == "cuda" else None
-    coef = torch.zeros(2 * m, dtype=torch.float32, device=dev)
+    coef = torch.zeros(2 * R, dtype=torch.float32, device=dev)
 
     def absmax(gv: torch.Tensor) -> torch.Tensor:
         return gv.abs().max().double() if gv.numel() else torch.zeros((), dtype=torch.float64,
@@ -152,11 +154,11 @@ def _lbfgs_minimize_impl(obj, maxiter: int = 100, m: int = 10, ftol: float = 1e7
             if order:
                 idx = np.array(order)
                 gamma, a, b = compact_coefficients(SY, YY, Sg, Yg, order)
-                cvec = np.zeros(2 * m)
+                cvec = np.zeros(2 * R)
                 cvec[idx] = -a
-                cvec[m + idx] = -gamma * b
+                cvec[R + idx] = -gamma * b
                 coef.copy_(torch.from_numpy(cvec.astype(np.float32)))
-                lincomb_(HS, 2 * m, coef, -gamma, g, d)
+                lincomb_(HS, 2 * R, coef, -gamma, g, d)
                 gd = -gamma * gg - float(a @ Sg[idx]) - gamma * float(b @ Yg[idx])
             else:
                 d.copy_(-g)
@@ -209,23 +211,23 @@ def _lbfgs_minimize_impl(obj, maxiter: int = 100, m: int = 10, ftol: float = 1e7
                     break
                 best = min(cands)[1]
             f_new, g_new, _ = cache[best]
-            # ---------------- update iterate and history
+            # ---------------- update iterate and history (new pair in the spare slot q)
+            q = min(set(range(R)) - set(order))
+            s_vec, y_vec = HS[q], HS[R + q]
             torch.mul(d, best, out=s_vec)
             x.add_(s_vec)
             torch.sub(g_new, g, out=y_vec)
             g_row.copy_(g_new)
             nit = k + 1
-            dv = dot(HX, 2 * m + 3, [s_vec, y_vec, g_row])  # (2m+3, 3)
+            dv = dot(HX, 2 * R + 1, [s_vec, y_vec, g_row])  # (2R+1, 3)
             host = red.reduce(sums=[dv], maxes=[absmax(g_new)])
-            dots = host[:-1].reshape(2 * m + 3, 3)
+            dots = host[:-1].reshape(2 * R + 1, 3)
             gmax = float(host[-1])
-            sy_new, yy_new = float(dots[2 * m, 1]), float(dots[2 * m + 1, 1])
-            gg = float(dots[2 * m + 2, 2])
-            inserted = sy_new > _EPS * yy_new and yy_new > 0
-            if inserted:
-                q = order.pop(0) if len(order) == m else min(set(range(m)) - set(order))
-                HS[q].copy_(s_vec)
-                HS[m + q].copy_(y_vec)
+            sy_new, yy_new = float(dots[q, 1]), float(dots[R + q, 1])
+            gg = float(dots[2 * R, 2])
+            if sy_new > _EPS * yy_new and yy_new > 0:  # accept: q joins, the oldest leaves
+                if len(order) == m:
+                    order.pop(0)
                 order.append(q)
                 for o in order:
                     if o == q:
@@ -233,13 +235,10 @@ def _lbfgs_minimize_impl(obj, maxiter: int = 100, m: int = 10, ftol: float = 1e7
                         YY[q, q] = yy_new
                     else:
                         SY[o, q] = dots[o, 1]          # s_o . y_new
-                        SY[q, o] = dots[m + o, 0]      # s_new . y_o
-                        YY[o, q] = YY[q, o] = dots[m + o, 1]
-            Sg[:] = dots[:m, 2]
-            Yg[:] = dots[m:2 * m, 2]
-            if inserted:
-                Sg[q] = dots[2 * m, 2]
-                Yg[q] = dots[2 * m + 1, 2]
+                        SY[q, o] = dots[R + o, 0]      # s_new . y_o
+                        YY[o, q] = YY[q, o] = dots[R + o, 1]
+            Sg[:] = dots[:R, 2]
+            Yg[:] = dots[R:2 * R, 2]
             f_old, f, g = f, f_new, g_new
             if callback is not None:
                 h0 = getattr(comm, "host_collectives", 0) if comm is not None else 0

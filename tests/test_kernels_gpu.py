@@ -270,6 +270,20 @@ def test_multi_dot_and_lincomb_kernels():
     assert torch.equal(md(A, r, B).cpu(), out)  # deterministic
     out1 = md(A, 7, B[:1]).cpu()
     torch.testing.assert_close(out1, ref[:7, :1], rtol=1e-5, atol=1e-3)
+    # every row-count / vector-count instantiation (1-3 rows per thread; 2/4/6/8 rows per
+    # wave; several row groups), float4 and scalar paths, against the fp64 product
+    r2, n2 = 40, 1_000_000  # float4 path (rows 16-byte aligned)
+    A2 = torch.randn(r2, n2, device=DEV)
+    B2 = [torch.randn(n2, device=DEV) for _ in range(4)]
+    ref2 = (A2.double() @ torch.stack(B2).double().T).cpu()
+    md2 = MultiDot(r2, n2, DEV)
+    for rows in (1, 2, 3, 4, 7, 8, 13, 16, 23, 24, 25, 32, 33, 40):
+        for nc in (1, 2, 3, 4):
+            got = md2(A2, rows, B2[:nc]).cpu()
+            torch.testing.assert_close(got, ref2[:rows, :nc], rtol=1e-5, atol=1e-3)
+    for rows in (1, 3, 13, 20):  # scalar path (n = 1_000_003: rows not 16-byte aligned)
+        got = md(A, rows, B).cpu()
+        torch.testing.assert_close(got, ref[:rows], rtol=1e-5, atol=1e-3)
     coef = torch.randn(r, device=DEV)
     y = torch.empty(n, device=DEV)
     lincomb_(A, r, coef, -0.5, B[0], y)
