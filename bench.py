@@ -67,6 +67,11 @@ def _args(argv=None):
                     help="fraction of populations (scattered by a hash) with a narrow true "
                          "sigma (bin width > 0.5 sigma: outside the Euler-Maclaurin forward's "
                          "range, evaluated by the per-edge path); the headline is 0")
+    ap.add_argument("--bounds", default="none", choices=["none", "both", "mixed"],
+                    help="box constraints (reference run_adam(param_bounds=...)): 'both' boxes "
+                         "every parameter around the start (truth inside), 'mixed' gives the "
+                         "a's a lower bound only and the log sigmas both bounds; the headline "
+                         "is unbounded")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--profile-phases", action="store_true")
     ap.add_argument("--no-count-launches", dest="count_launches", action="store_false",
@@ -123,6 +128,18 @@ def launch(args, argv) -> int:
     return subprocess.run(cmd, env=env).returncode
 
 
+def bench_bounds(args, data):
+    """``(P, 2)`` box constraints for ``--bounds`` (None: unbounded), around the start."""
+    if args.bounds == "none":
+        return None
+    import torch
+    g = data["guess"].detach()
+    pb = torch.stack([g - 1.0, g + 0.5], 1)
+    if args.bounds == "mixed":
+        pb[0::2, 1] = float("inf")  # a: lower bound only
+    return pb
+
+
 def time_placement(placement, args, comm, dev, sync):
     """Build the data and engine for one placement, warm up, time ``args.steps`` steps.
 
@@ -145,7 +162,7 @@ def time_placement(placement, args, comm, dev, sync):
         engine.timer = PhaseTimer(True)
     count = args.count_launches and dev.type == "cuda"
     engine.setup(data["guess"], nsteps=args.warmup + args.steps + (2 if count else 0),
-                 learning_rate=args.lr, history=history)
+                 learning_rate=args.lr, history=history, param_bounds=bench_bounds(args, data))
     sync()
     setup_s = time.perf_counter() - t_setup
 
@@ -304,6 +321,7 @@ def main(argv=None):
             "chunks": head["chunks"],
             "layout": head["layout"],
             "narrow_frac": args.narrow_frac,
+            "bounds": args.bounds,
             "per_edge_groups": head["fallback_groups"],
             "device_ops_per_step": head["device_ops_per_step"],
             "autotune": head["autotune"],

@@ -218,7 +218,8 @@ __global__ __launch_bounds__(kThreads, MG_FWD_MINWAVES) void smf_fwd_kernel(
   int bid = blockIdx.x, nblk = gridDim.x;
   if constexpr (XS) {
     if (bid < xs.blocks) {
-      twoshot_block_fused(xs.a, bid, xs.blocks);
+      __shared__ int xs_lds[2];  // 8 bytes: this kernel's occupancy is set by its VGPRs
+      twoshot_block_fused(xs.a, bid, xs.blocks, xs_lds);
       return;
     }
     bid -= xs.blocks;
@@ -585,8 +586,12 @@ __device__ __forceinline__ float2 pop_grad(float2 th, float A, float B) {
 }
 
 // Pipelined update (see smf_fwd_lanes_kernel<..., UPD>): the previous step's residual
-// VJP + unbounded Adam of a population run in the lane that is about to evaluate the
-// population's halos at the new parameters.
+// VJP + Adam of a population run in the lane that is about to evaluate the population's
+// halos at the new parameters.  BND (bounded fits, reference multigrad/adam.py:133-189):
+// Adam runs on the unbounded coordinates u (indexed like m, v), the gradient is scaled by
+// the diagonal dp/du (at u, or at the old p with the reference's legacy Jacobian, SURVEY
+// Q1) and the forward evaluates p = T^-1(u) (csrc/adam.h); the bound kind of a coordinate
+// follows from which of its bounds are finite.
 __global__ void smf_advance_step_kernel(int* step);
 
 struct LanesUpdate {
@@ -600,7 +605,44 @@ struct LanesUpdate {
   const int* step;      // device step counter (read when host_step < 0)
   int host_step;
   float lr, b1, b2, eps;
+  float2* u;            // BND: unbounded coordinates (indexed like m, v)
+  const float2* lo;     // BND: bounds, -inf / +inf where absent (indexed like m, v)
+  const float2* hi;
+  int legacy;           // BND: dp/du at the old p (reference quirk Q1)
 };
+
+// bound kind from the finite bounds (csrc/adam.h BoundKind)
+__device__ __forceinline__ int8_t bound_kind(float lo, float hi) {
+  const bool l = __builtin_isfinite(lo), h = __builtin_isfinite(hi);
+  return l ? (h ? kBoth : kLow) : (h ? kHigh : kNone);
+}
+
+// dp/du and p = T^-1(u) of csrc/adam.h with hardware reciprocals (v_rcp / v_rsq, ~1 ulp)
+// instead of IEEE divisions (~10 VALU ops each, three per coordinate): the update runs in the
+// VALU-bound forward, where they measured 480 vs 440 us per step (the stand-alone bounded
+// Adam keeps the exact forms; the two schedules agree to a few ulps, as the unbounded
+// pipelined update's reciprocal bias corrections do)
+__device__ __forceinline__ float dpdu_fast(float at, float lo, float hi, int8_t k) {
+  if (k == kBoth) {
+    const float r = at * __builtin_amdgcn_rcpf((hi - lo) * (1.0f / kPi));
+    return __builtin_amdgcn_rcpf(fmaf(r, r, 1.0f));
+  }
+  if (k == kLow || k == kHigh) {
+    const float q = at * __builtin_amdgcn_rsqf(fmaf(at, at, 4.0f));
+    return 0.5f * (k == kLow ? 1.0f + q : 1.0f - q);
+  }
+  return 1.0f;
+}
+
+__device__ __forceinline__ float inv_transform_fast(float u, float lo, float hi, int8_t k) {
+  if (k == kBoth) {
+    const float s = (hi - lo) * (1.0f / kPi);
+    return fmaf(s, atanf(u * __builtin_amdgcn_rcpf(s)), (hi + lo) * 0.5f);
+  }
+  if (k == kLow) return 0.5f * (2.0f * lo + u + __builtin_amdgcn_sqrtf(fmaf(u, u, 4.0f)));
+  if (k == kHigh) return 0.5f * (2.0f * hi + u - __builtin_amdgcn_sqrtf(fmaf(u, u, 4.0f)));
+  return u;
+}
 
 // Segmented-scan combine: (flag, A, B) pairs.
 struct Seg {
@@ -1247,19 +1289,21 @@ __global__ __launch_bounds__(kThreads, MG_VJP_REC_MINWAVES) void smf_vjp_tiles_r
   // XS (fused exchange): workgroups [0, xs.blocks) run the two-shot exchange of the
   // previous parameter chunk (its gradient is complete: the launch that wrote it ended
   // before this one), the rest one tile each
+  // LDS (20 KB, so 8 workgroups fit a CU): per-halo contributions (later the per-population
+  // results) and local population ids (later the head partials and their successors); the
+  // exchange workgroups of the XS variant borrow its first 8 bytes for their flags, so the
+  // fused kernel keeps the same 20 KB and 8 workgroups per CU
+  __shared__ __attribute__((aligned(16))) char smem[kTileHalos * (sizeof(float2) + sizeof(int16_t))];
   int tb = blockIdx.x;
   if constexpr (XS) {
     if (tb < xs.blocks) {
-      twoshot_block_fused(xs.a, tb, xs.blocks);
+      twoshot_block_fused(xs.a, tb, xs.blocks, reinterpret_cast<int*>(smem));
       return;
     }
     tb -= xs.blocks;
   }
   using EP = EdgePairs<NB>;
   constexpr int M = EP::NP / 2;
-  // LDS (20 KB, so 8 workgroups fit a CU): per-halo contributions (later the per-population
-  // results) and local population ids (later the head partials and their successors)
-  __shared__ __attribute__((aligned(16))) char smem[kTileHalos * (sizeof(float2) + sizeof(int16_t))];
   const Tile t = tiles[tb];
   const int tid = threadIdx.x;
   if (t.slot >= 0) {  // partial tile (one giant population): the per-edge block reduction
@@ -1658,7 +1702,8 @@ __device__ __attribute__((noinline)) LaneGroupSums<NB> lanes_group_exact(
 // takes it: profiles/em_forward/, 2276-2291 vs 2204-2210 steps/s); 2 = LIST: the fix-up
 // launch that follows, over the listed groups only (EM + per-edge fallback, residuals and
 // its own slab rows), whose last workgroup resets the list for the next launch.
-template <int NB, bool LOGSIG, bool REL, bool RESID, bool UPD = false, int LMODE = 0>
+template <int NB, bool LOGSIG, bool REL, bool RESID, bool UPD = false, int LMODE = 0,
+          bool BND = false>
 __global__ __launch_bounds__(kThreads, MG_LANES_MINWAVES) void smf_fwd_lanes_kernel(
     const float* __restrict__ xi, const int32_t* __restrict__ slot_pop,
     const int64_t* __restrict__ group_base, const int32_t* __restrict__ group_len,
@@ -1667,6 +1712,7 @@ __global__ __launch_bounds__(kThreads, MG_LANES_MINWAVES) void smf_fwd_lanes_ker
     const int32_t* __restrict__ wave_start, int* __restrict__ queues, int nq,
     LanesUpdate upd = LanesUpdate{}, int* __restrict__ defer = nullptr, EpiArgs epi = EpiArgs{}) {
   static_assert(!UPD || RESID, "the pipelined update reads the residuals it overwrites");
+  static_assert(!BND || UPD, "bounds belong to the pipelined update");
   static_assert(LMODE == 0 || LMODE == 4 || (RESID && MG_FWD_EM && MG_LANES_EP && !REL),
                 "deferral: EM residual forwards");
   static_assert(LMODE != 2 || !UPD, "the fix-up launch evaluates updated groups");
@@ -1786,7 +1832,8 @@ __global__ __launch_bounds__(kThreads, MG_LANES_MINWAVES) void smf_fwd_lanes_ker
   // the group is loaded -- no VGPRs (the 64-bit per-lane pointers of a register load spill
   // this kernel), and they travel with the theta gather and the first halos, so the group
   // transition still costs one memory round trip.
-  constexpr int kUR = UPD ? 2 * (NB + 1) + 4 : 1;  // rows: G[NB+1], W[NB+1], m.x m.y v.x v.y
+  // rows: G[NB+1], W[NB+1], m.x m.y v.x v.y (BND: + u.x u.y lo.x lo.y hi.x hi.y)
+  constexpr int kUR = UPD ? 2 * (NB + 1) + 4 + (BND ? 6 : 0) : 1;
   float* ubuf = nullptr;
   const float* uh = nullptr;  // the edge weights, in LDS (a vector load of them would be
                               // counted by vmcnt and make every group wait for its stores)
@@ -1809,6 +1856,17 @@ __global__ __launch_bounds__(kThreads, MG_LANES_MINWAVES) void smf_fwd_lanes_ker
       __builtin_amdgcn_global_load_lds(mp + 1, ubuf + (NR + 1) * kWave, 4, 0, 0);
       __builtin_amdgcn_global_load_lds(vp, ubuf + (NR + 2) * kWave, 4, 0, 0);
       __builtin_amdgcn_global_load_lds(vp + 1, ubuf + (NR + 3) * kWave, 4, 0, 0);
+      if constexpr (BND) {
+        const float* up = reinterpret_cast<const float*>(upd.u + j);
+        const float* lp = reinterpret_cast<const float*>(upd.lo + j);
+        const float* hp = reinterpret_cast<const float*>(upd.hi + j);
+        __builtin_amdgcn_global_load_lds(up, ubuf + (NR + 4) * kWave, 4, 0, 0);
+        __builtin_amdgcn_global_load_lds(up + 1, ubuf + (NR + 5) * kWave, 4, 0, 0);
+        __builtin_amdgcn_global_load_lds(lp, ubuf + (NR + 6) * kWave, 4, 0, 0);
+        __builtin_amdgcn_global_load_lds(lp + 1, ubuf + (NR + 7) * kWave, 4, 0, 0);
+        __builtin_amdgcn_global_load_lds(hp, ubuf + (NR + 8) * kWave, 4, 0, 0);
+        __builtin_amdgcn_global_load_lds(hp + 1, ubuf + (NR + 9) * kWave, 4, 0, 0);
+      }
     }
   };
   // previous step's VJP of the current group's populations from the staged residuals, then
@@ -1827,12 +1885,30 @@ __global__ __launch_bounds__(kThreads, MG_LANES_MINWAVES) void smf_fwd_lanes_ker
         const int64_t j = c_cur - upd.unit_offset;
         float2 mm = make_float2(ubuf[NR * kWave + lane], ubuf[(NR + 1) * kWave + lane]);
         float2 vv = make_float2(ubuf[(NR + 2) * kWave + lane], ubuf[(NR + 3) * kWave + lane]);
-        mm.x = (1.0f - upd.b1) * gr.x + upd.b1 * mm.x;
-        mm.y = (1.0f - upd.b1) * gr.y + upd.b1 * mm.y;
-        vv.x = (1.0f - upd.b2) * (gr.x * gr.x) + upd.b2 * vv.x;
-        vv.y = (1.0f - upd.b2) * (gr.y * gr.y) + upd.b2 * vv.y;
-        th.x -= upd.lr * (mm.x * ubc1) * __builtin_amdgcn_rcpf(__builtin_amdgcn_sqrtf(vv.x * ubc2) + upd.eps);
-        th.y -= upd.lr * (mm.y * ubc1) * __builtin_amdgcn_rcpf(__builtin_amdgcn_sqrtf(vv.y * ubc2) + upd.eps);
+        if constexpr (BND) {
+          float2 uu = make_float2(ubuf[(NR + 4) * kWave + lane], ubuf[(NR + 5) * kWave + lane]);
+          const float2 lo = make_float2(ubuf[(NR + 6) * kWave + lane], ubuf[(NR + 7) * kWave + lane]);
+          const float2 hi = make_float2(ubuf[(NR + 8) * kWave + lane], ubuf[(NR + 9) * kWave + lane]);
+          const int8_t kx = bound_kind(lo.x, hi.x), ky = bound_kind(lo.y, hi.y);
+          const float gx = gr.x * dpdu_fast(upd.legacy ? th.x : uu.x, lo.x, hi.x, kx);
+          const float gy = gr.y * dpdu_fast(upd.legacy ? th.y : uu.y, lo.y, hi.y, ky);
+          mm.x = (1.0f - upd.b1) * gx + upd.b1 * mm.x;
+          mm.y = (1.0f - upd.b1) * gy + upd.b1 * mm.y;
+          vv.x = (1.0f - upd.b2) * (gx * gx) + upd.b2 * vv.x;
+          vv.y = (1.0f - upd.b2) * (gy * gy) + upd.b2 * vv.y;
+          uu.x -= upd.lr * (mm.x * ubc1) * __builtin_amdgcn_rcpf(__builtin_amdgcn_sqrtf(vv.x * ubc2) + upd.eps);
+          uu.y -= upd.lr * (mm.y * ubc1) * __builtin_amdgcn_rcpf(__builtin_amdgcn_sqrtf(vv.y * ubc2) + upd.eps);
+          th.x = inv_transform_fast(uu.x, lo.x, hi.x, kx);
+          th.y = inv_transform_fast(uu.y, lo.y, hi.y, ky);
+          upd.u[j] = uu;
+        } else {
+          mm.x = (1.0f - upd.b1) * gr.x + upd.b1 * mm.x;
+          mm.y = (1.0f - upd.b1) * gr.y + upd.b1 * mm.y;
+          vv.x = (1.0f - upd.b2) * (gr.x * gr.x) + upd.b2 * vv.x;
+          vv.y = (1.0f - upd.b2) * (gr.y * gr.y) + upd.b2 * vv.y;
+          th.x -= upd.lr * (mm.x * ubc1) * __builtin_amdgcn_rcpf(__builtin_amdgcn_sqrtf(vv.x * ubc2) + upd.eps);
+          th.y -= upd.lr * (mm.y * ubc1) * __builtin_amdgcn_rcpf(__builtin_amdgcn_sqrtf(vv.y * ubc2) + upd.eps);
+        }
         upd.m[j] = mm;
         upd.v[j] = vv;
         upd.theta_w[c_cur] = th;
@@ -2885,13 +2961,16 @@ int64_t smf_forward_lanes(torch::Tensor xi, torch::Tensor slot_pop, torch::Tenso
     }
   };
   if (update.has_value()) {
-    // pipelined update: tensors [h, m, v, step(int32[2]), traj (or empty)]; scalars
-    // [unit_offset, host_step, lr, b1, b2, eps, traj_stride]
+    // pipelined update: tensors [h, m, v, step(int32[2]), traj (or empty)] (+ [u, lo, hi]
+    // for bounded fits); scalars [unit_offset, host_step, lr, b1, b2, eps, traj_stride
+    // (, defer_advance (, legacy))]
     const auto& U = *update;
-    TORCH_CHECK(U.size() == 5 && (update_scalars.size() == 7 || update_scalars.size() == 8),
-                "update: 5 tensors, 7 scalars (+ defer_advance)");
+    TORCH_CHECK((U.size() == 5 || U.size() == 8) && update_scalars.size() >= 7 &&
+                    update_scalars.size() <= 9,
+                "update: 5 tensors (+ u, lo, hi), 7 scalars (+ defer_advance, legacy)");
     // defer_advance: the caller advances the device step counter itself (the epilogue)
-    const bool defer_advance = update_scalars.size() == 8 && update_scalars[7] != 0.0;
+    const bool defer_advance = update_scalars.size() >= 8 && update_scalars[7] != 0.0;
+    const bool bnd = U.size() == 8;
     TORCH_CHECK(has_resid, "the pipelined update needs the residual buffer");
     check_dev(U[0], "h", at::kFloat);
     check_dev(U[1], "m", at::kFloat);
@@ -2915,6 +2994,41 @@ int64_t smf_forward_lanes(torch::Tensor xi, torch::Tensor slot_pop, torch::Tenso
     TORCH_CHECK(u.unit_offset >= 0 && 2 * (u.unit_offset + U[1].numel() / 2) <= theta.numel(),
                 "bad unit offset");
     u.step = U[3].data_ptr<int>();
+    u.u = nullptr;
+    u.lo = u.hi = nullptr;
+    u.legacy = update_scalars.size() >= 9 && update_scalars[8] != 0.0;
+    if (bnd) {
+      // bounded fits: the Euler-Maclaurin / per-edge residual forwards of the population
+      // models (log10 sigma, absolute tails)
+      TORCH_CHECK(log_sigma && (lcall || ledge), "the bounded pipelined update needs the "
+                  "log-sigma Euler-Maclaurin or per-edge residual forward");
+      for (int i = 5; i < 8; ++i) {
+        check_dev(U[i], i == 5 ? "u" : i == 6 ? "lo" : "hi", at::kFloat);
+        TORCH_CHECK(U[i].numel() == U[1].numel(), "u / lo / hi must be shaped like m");
+      }
+      u.u = reinterpret_cast<float2*>(U[5].data_ptr<float>());
+      u.lo = reinterpret_cast<const float2*>(U[6].data_ptr<float>());
+      u.hi = reinterpret_cast<const float2*>(U[7].data_ptr<float>());
+      MG_DISPATCH_NB(nbp, {
+        if (lcall) {
+          hipLaunchKernelGGL((smf_fwd_lanes_kernel<NB, true, false, true, true, kLanesMainMode, true>),
+                             dim3(nblocks), dim3(kThreads), 0, stream, xi.data_ptr<float>(),
+                             slot_pop.data_ptr<int32_t>(), group_base.data_ptr<int64_t>(),
+                             group_len.data_ptr<int32_t>(), order, tp, g0, g1, b,
+                             slab.data_ptr<float>(), rp, ws, qp, nq, u, dmain, epi_main);
+        } else {
+          hipLaunchKernelGGL((smf_fwd_lanes_kernel<NB, true, false, true, true, 4, true>),
+                             dim3(nblocks), dim3(kThreads), 0, stream, xi.data_ptr<float>(),
+                             slot_pop.data_ptr<int32_t>(), group_base.data_ptr<int64_t>(),
+                             group_len.data_ptr<int32_t>(), order, tp, g0, g1, b,
+                             slab.data_ptr<float>(), rp, ws, qp, nq, u, tk, epi_main);
+        }
+      });
+      fixup();
+      if (u.host_step < 0 && !defer_advance)
+        hipLaunchKernelGGL(smf_advance_step_kernel, dim3(1), dim3(1), 0, stream, U[3].data_ptr<int>());
+      return nblocks + fixb;
+    }
     MG_DISPATCH_NB(nbp, {
       with_bool(log_sigma, [&](auto LS) {
         if (lmode || lcall) {

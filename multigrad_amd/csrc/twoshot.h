@@ -48,8 +48,10 @@ constexpr int kTsThreads = 256;
 // The exchange as workgroups [0, nblk) of the calling grid (bid = this workgroup's index in
 // that range).  Every workgroup of the range must call it; it returns when this
 // workgroup's share is done (the last one returns when every rank's slice has landed).
+// `lds`: two ints of LDS for the block-wide flags (lent by the caller: the fused VJP sits at
+// exactly 20 KiB so that 8 workgroups fit a CU, and a __shared__ here would add to it).
 template <int MODE, int PB = kXMaxRanks>
-__device__ __forceinline__ void twoshot_block(const TwoShotArgs& a, int bid, int nblk) {
+__device__ __forceinline__ void twoshot_block(const TwoShotArgs& a, int bid, int nblk, int* lds) {
   static_assert(kXMaxRanks % PB == 0, "peer batches must tile the rank limit");
   static_assert(MODE >= 0 && MODE <= 5, "two-shot mode");
   constexpr bool ADAM = MODE >= 1 && MODE <= 3;
@@ -65,7 +67,7 @@ __device__ __forceinline__ void twoshot_block(const TwoShotArgs& a, int bid, int
   // my gradient is complete: the VJP's stores to the uncached buffer were acknowledged
   // before that launch ended, and this launch is ordered after it
   if (bid == 0 && (int)threadIdx.x < a.size) uc_signal(ts_gflag(a.f.base[threadIdx.x]) + a.rank, seq);
-  const int bad = ts_wait_all(ts_gflag(me), a.size, seq, a.err, a.ticks);
+  const int bad = ts_wait_all(ts_gflag(me), a.size, seq, a.err, a.ticks, lds + 1);
   const float bc1 = 1.0f - powf(a.b1, (float)(st + 1));
   const float bc2 = 1.0f - powf(a.b2, (float)(st + 1));
   float* trow = a.traj ? a.traj + (int64_t)(st + 1) * a.traj_stride : nullptr;
@@ -142,7 +144,7 @@ __device__ __forceinline__ void twoshot_block(const TwoShotArgs& a, int bid, int
   // peer's slice has landed here
   uc_release();
   __syncthreads();
-  __shared__ int last;
+  int& last = lds[0];
   if (threadIdx.x == 0) {
     const unsigned tk = atomicAdd(ts_ticket(me), 1u);
     last = tk == (unsigned)nblk - 1;
@@ -151,7 +153,7 @@ __device__ __forceinline__ void twoshot_block(const TwoShotArgs& a, int bid, int
   if (!last) return;
   if (threadIdx.x == 0) __hip_atomic_store(ts_ticket(me), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if ((int)threadIdx.x < a.size) uc_signal(ts_tflag(a.f.base[threadIdx.x]) + a.rank, seq);
-  ts_wait_all(ts_tflag(me), a.size, seq, a.err, a.ticks);
+  ts_wait_all(ts_tflag(me), a.size, seq, a.err, a.ticks, lds + 1);
   if (threadIdx.x == 0) {
     __hip_atomic_store(a.seq, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (a.host_step < 0) __hip_atomic_store(a.step, st + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -161,8 +163,9 @@ __device__ __forceinline__ void twoshot_block(const TwoShotArgs& a, int bid, int
 
 // The exchange carried by a compute kernel (fused exchange): unbounded Adam only (the
 // bounded modes launch on their own, see smf_forward / smf_vjp), peers 4 at a time.
-__device__ __forceinline__ void twoshot_block_fused(const TwoShotArgs& a, int bid, int nblk) {
-  twoshot_block<1, 4>(a, bid, nblk);
+__device__ __forceinline__ void twoshot_block_fused(const TwoShotArgs& a, int bid, int nblk,
+                                                    int* lds) {
+  twoshot_block<1, 4>(a, bid, nblk, lds);
 }
 
 // Packed launch arguments of one exchange (xgmi_twoshot_pack -> the fused kernels' host

@@ -145,10 +145,11 @@ __device__ __forceinline__ unsigned* ts_ticket(char* b) {
 // Threads t < size of the calling block wait until flag[t] >= seq (monotonic sequence
 // numbers, wrap-safe difference); returns 1 (and raises *err) on a timeout -- at once when
 // *err is already raised (a protocol out of step until reset(): no second timeout).  Every
-// thread of the block must call it.
+// thread of the block must call it.  `to`: one int of LDS (the caller's, so a kernel that
+// carries the exchange can lend it from its own LDS instead of growing its footprint).
 __device__ __forceinline__ int ts_wait_all(unsigned* flags, int size, unsigned seq, int* err,
-                                           long long timeout_ticks) {
-  __shared__ int to;
+                                           long long timeout_ticks, int* to_lds) {
+  int& to = *to_lds;
   if (threadIdx.x == 0) to = 0;
   __syncthreads();
   if ((int)threadIdx.x < size) {

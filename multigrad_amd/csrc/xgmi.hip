@@ -236,7 +236,8 @@ std::string device_pci_bus_id() {
 // owned slice instead of hanging.
 template <int MODE>
 __global__ __launch_bounds__(kTsThreads) void xgmi_twoshot_kernel(TwoShotArgs a) {
-  twoshot_block<MODE>(a, blockIdx.x, gridDim.x);
+  __shared__ int lds[2];
+  twoshot_block<MODE>(a, blockIdx.x, gridDim.x, lds);
 }
 
 static XgmiPeers peers_of(const std::vector<int64_t>& v) {

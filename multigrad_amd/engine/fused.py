@@ -484,11 +484,12 @@ class FusedAdamEngine:
             self.ts_blocks = int(os.environ.get("MULTIGRAD_TWOSHOT_BLOCKS", "256"))
         self.pending = False
         ok = getattr(md, "engine_pipeline_ok", None)
+        pchunk = self.rank if self.owner else None
         self.pipeline = bool(
-            _env_flag("MULTIGRAD_PIPELINE", True) and self.fuse_vjp_adam and bounds is None
+            _env_flag("MULTIGRAD_PIPELINE", True) and self.fuse_vjp_adam
             and (self.owner or (not self.zero and self.C == 1 and self.size == 1))
             and ok is not None and hasattr(md, "engine_forward_update_chunk")
-            and ok(self.rank if self.owner else None))
+            and (ok(pchunk) if bounds is None else ok(pchunk, bounded=True)))
         # a step can be captured when every collective in it is a peer-memory kernel with
         # its sequence number in device memory (one-shot sumstats, two-shot gradient) --
         # RCCL/gloo calls are not captured
@@ -897,7 +898,10 @@ class FusedAdamEngine:
         if self.pending:
             self.pending = False
             idx = self.step_host - 1
-            if self.owner:
+            ok = True
+            if self.bounds is not None:
+                self._drain_bounded(idx)
+            elif self.owner:
                 a, b = self.own_range
                 tl = self._tl()
                 tb = None if tl is None else tl.reshape(-1)
@@ -907,6 +911,29 @@ class FusedAdamEngine:
                 ok = self._fused_vjp_adam(None, 0, hb, self.P if hb is not None else 0,
                                           host_step=self._hstep(idx))
             assert ok, "pipelined engine lost its fused VJP + Adam path"
+
+    def _drain_bounded(self, idx: int) -> None:
+        """The pending update of step ``idx`` of a bounded pipelined fit: residual VJP and
+        the bounded Adam kernel (csrc/adam.hip; the end of a run or a checkpoint)."""
+        md = self.model
+        hs = self._hstep(idx)
+        if self.owner:
+            a, b = self.own_range
+            md.engine_vjp_into(self.theta, self.h, self.grad, chunk=self.rank)
+            tl = self._tl()
+            tb = None if tl is None else tl.reshape(-1)
+            adam_step_(self.u_loc, self.m, self.v, self.grad[a:b], self.theta[a:b],
+                       self.step_dev[0], self.lr, self.b1, self.b2, self.eps, self.bounds_loc,
+                       self.legacy, traj_base=tb, traj_stride=(b - a) if tb is not None else 0,
+                       host_step=hs)
+            return
+        md.engine_vjp_into(self.theta, self.h, self.grad, chunk=None)
+        hb = self._hb()
+        P, bnd = self.P, self.bounds
+        adam_step_(self.u[:P], self.m[:P], self.v[:P], self.grad[:P], self.theta[:P],
+                   self.step_dev[0], self.lr, self.b1, self.b2, self.eps,
+                   Bounds(bnd.lo[:P], bnd.hi[:P], bnd.kind[:P]), self.legacy, traj_base=hb,
+                   traj_stride=P if hb is not None else 0, host_step=hs)
 
     # ------------------------------------------------------------------ one step
     def _update_args(self, step_idx: int) -> dict:
@@ -920,10 +947,15 @@ class FusedAdamEngine:
             a = 0
             traj = self._hb()
             stride = self.P
-        return dict(h=self.h, m=self.m, v=self.v, unit_offset=a // self.upp,
+        args = dict(h=self.h, m=self.m, v=self.v, unit_offset=a // self.upp,
                     step=self.step_dev[0], host_step=self._hstep(step_idx), lr=self.lr,
                     b1=self.b1, b2=self.b2, eps=self.eps, traj=traj,
                     traj_stride=stride if traj is not None else 0)
+        if self.bounds is not None:  # bounded: Adam on u (indexed like m, v), p = T^-1(u)
+            bnd = self.bounds_loc if self.owner else self.bounds
+            args.update(u=self.u_loc if self.owner else self.u, lo=bnd.lo, hi=bnd.hi,
+                        legacy=self.legacy)
+        return args
 
     def _forward_loss(self, update: bool = False):
         md = self.model
@@ -1362,6 +1394,10 @@ class FusedAdamEngine:
     def load_state_dict(self, st: dict) -> int:
         """Restore a :meth:`state_dict` into a :meth:`setup` engine of the same shape;
         returns the step to continue from."""
+        # finish this engine's in-flight work first: a pending fused exchange (the last chunk's
+        # reduce-scatter -> Adam -> all-gather, carried by the next launch) or a pending
+        # pipelined update would otherwise run on top of the loaded state
+        self.drain()
         mode = "owner" if self.owner else "zero" if self.zero else "replicated"
         if st["mode"] != mode or st["size"] != self.size or st["P"] != self.P or \
                 list(st["pb"]) != list(self.pb):

@@ -338,11 +338,15 @@ class PopulationSMFModel(OnePointModel):
         for c in chunks:
             prepare_forward(self.shard, self.bins, True, c)
 
-    def engine_pipeline_ok(self, chunk=None) -> bool:
+    def engine_pipeline_ok(self, chunk=None, bounded: bool = False) -> bool:
         """Whether :meth:`engine_forward_chunk` can also apply the previous step's VJP and
-        Adam update (lanes layout on the GPU, internal order, no split populations)."""
+        Adam update (lanes layout on the GPU, internal order, no split populations);
+        ``bounded``: the bounded form (box-constrained Adam in u-space), which needs the
+        Euler-Maclaurin / per-edge residual forward (uniform bins, absolute tails)."""
         sh = self.shard
         if sh.device.type != "cuda" or self._engine_order() != "internal":
+            return False
+        if bounded and (self.bins.rel_tail or self.bins.delta <= 0):
             return False
         k0, k1 = (0, sh.giant.shape[0]) if chunk is None else \
             (sh.chunk_giant[chunk], sh.chunk_giant[chunk + 1])

@@ -563,6 +563,9 @@ def smf_forward_slab(theta: torch.Tensor, shard: PopulationShard, bins: SmfBins,
             usc = [float(u["unit_offset"]), float(-1 if u.get("host_step") is None else u["host_step"]),
                    float(u["lr"]), float(u["b1"]), float(u["b2"]), float(u["eps"]),
                    float(u.get("traj_stride", 0)), float(bool(u.get("defer_advance", False)))]
+            if u.get("u") is not None:  # bounded: Adam on u, p = T^-1(u) (csrc/adam.h)
+                upd += [u["u"], u["lo"], u["hi"]]
+                usc.append(float(bool(u.get("legacy", False))))
         et, es, ep = [], [], []
         if epilogue is not None:  # the sumstat epilogue folded into this launch sequence
             e = epilogue

@@ -56,6 +56,17 @@ class Bounds:
     def from_spec(param_bounds, ndim: int, device=None, dtype=torch.float32) -> Optional["Bounds"]:
         if param_bounds is None:
             return None
+        if isinstance(param_bounds, (np.ndarray, torch.Tensor)) and \
+                param_bounds.dtype not in (object, np.object_) and tuple(param_bounds.shape) == (ndim, 2):
+            # numeric (ndim, 2) array: vectorised (a 1e7-row Python loop takes seconds);
+            # non-finite entries mark an absent side, as in the list form
+            arr = torch.as_tensor(param_bounds).to(device=device, dtype=torch.float64)
+            lo_t, hi_t = arr[:, 0], arr[:, 1]
+            fl, fh = torch.isfinite(lo_t), torch.isfinite(hi_t)
+            kind = torch.where(fl & fh, KIND_BOTH, torch.where(fl, KIND_LOW, torch.where(
+                fh, KIND_HIGH, KIND_NONE))).to(torch.int8)
+            return Bounds(torch.where(fl, lo_t, -math.inf).to(dtype),
+                          torch.where(fh, hi_t, math.inf).to(dtype), kind)
         if hasattr(param_bounds, "tolist"):
             param_bounds = param_bounds.tolist()
         pb = list(param_bounds)

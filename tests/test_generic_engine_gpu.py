@@ -397,6 +397,7 @@ def test_graph_engine_replays_after_eager_steps_with_syncs(keyed):
     ref = m.run_adam(guess, nsteps=len(sched), learning_rate=1e-3, use_engine=False, **kw)
     eng = GraphAdamEngine(m, graph=True)
     eng.setup(guess, nsteps=len(sched), learning_rate=1e-3, **kw)
+    eng.step_replay = True  # direct calls replay: the caller's kernels are in eng.stream()
     scratch = torch.zeros(1, device=DEV)
     for mode in sched:
         eng.use_graph = mode == "g"
@@ -435,3 +436,39 @@ def test_engines_launch_on_their_own_stream():
     tf = feng.run_adam(data["guess"], nsteps=4, learning_rate=1e-3, callback=cb)
     assert seen and all(s == feng._es for s in seen)
     assert torch.isfinite(tf).all()
+
+
+@pytest.mark.parametrize("engine", ["generic", "fused"])
+def test_direct_steps_with_default_stream_work_match_eager(engine):
+    """a user loop of direct step() calls with its own kernels on the legacy default
+    stream and a host synchronisation between the calls -- the schedule after which a graph
+    replay computes garbage on this HIP runtime -- gives the eager trajectory bit for bit,
+    because direct calls launch eagerly (step_replay off); steps() still replays."""
+    from multigrad_amd.engine.fused import FusedAdamEngine
+    from multigrad_amd.engine.generic import GraphAdamEngine
+    from multigrad_amd.models.population import PopulationSMFModel, make_population_data
+    if engine == "generic":
+        m, guess = _torch_pop()
+        mk = lambda g: GraphAdamEngine(m, graph=g)  # noqa: E731
+    else:
+        data = make_population_data(num_params=4000, num_halos=100_000, seed=3, device=DEV)
+        m = PopulationSMFModel(aux_data=data)
+        m.set_target_from_truth()
+        guess = data["guess"]
+        mk = lambda g: FusedAdamEngine(m, graph=g)  # noqa: E731
+    n = 12
+    ref = mk(False)
+    ref.setup(guess, nsteps=n, learning_rate=1e-3)
+    ref.steps(n)
+    want = ref.trajectory().cpu()
+    eng = mk(True)
+    eng.setup(guess, nsteps=n, learning_rate=1e-3)
+    assert eng.use_graph and not eng.step_replay
+    scratch = torch.zeros(1, device=DEV)
+    eng.steps(4)                       # replays (a graph now exists)
+    for _ in range(n - 4):
+        eng.step()                     # direct calls: eager launches
+        scratch.add_(1)                # the caller's own kernel on the default stream
+        torch.cuda.synchronize()
+    got = eng.trajectory().cpu()
+    torch.testing.assert_close(got, want, rtol=1e-6, atol=1e-7)

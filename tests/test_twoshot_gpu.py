@@ -448,3 +448,42 @@ def test_engine_hashed_fused_exchange_matches_serial(size, chunks):
         ref = run_distributed(_engine_hashed, 2, False, False, chunks, "auto", None, "off",
                               timeout=600)
         np.testing.assert_array_equal(fus[0][0], ref[0][0])
+
+
+def _load_midrun(rank, size):
+    os.environ["MULTIGRAD_TWOSHOT_FUSED"] = "on"
+    os.environ["MULTIGRAD_TWOSHOT_SIDE_STREAM"] = "off"
+    os.environ["MULTIGRAD_CHUNKS"] = "2"
+    import multigrad_amd as mg
+    from multigrad_amd.engine.fused import FusedAdamEngine
+    from multigrad_amd.models.population import PopulationSMFModel, make_population_data
+    comm = mg.get_world_comm()
+    dev = torch.device("cuda", 0)
+    data = make_population_data(6000, 300_000, seed=31, comm=comm, device=dev, placement="hashed")
+    model = PopulationSMFModel(aux_data=data, comm=comm)
+    model.set_target_from_truth()
+    a = FusedAdamEngine(model)
+    a.setup(data["guess"], nsteps=8, learning_rate=1e-3)
+    assert a.ts_fused and a.C == 2
+    a.steps(3)
+    saved = a.state_dict()          # drains: the state after exactly 3 steps
+    a.steps(2)                      # leaves the last chunk's exchange pending ...
+    assert a._x_pending is not None
+    a.load_state_dict(saved)        # ... which must not run on top of the loaded state
+    a.steps(2)
+    ta = a.trajectory()[:6].cpu().numpy()
+    a.close()
+    b = FusedAdamEngine(model)
+    b.setup(data["guess"], nsteps=8, learning_rate=1e-3)
+    b.load_state_dict(saved)
+    b.steps(2)
+    tb = b.trajectory()[:6].cpu().numpy()
+    b.close()
+    return ta, tb
+
+
+def test_load_state_dict_mid_run_discards_nothing_pending():
+    """loading a checkpoint into an engine with a pending fused exchange gives the
+    same continuation as a fresh engine resumed from that checkpoint."""
+    for ta, tb in run_distributed(_load_midrun, 2, timeout=600):
+        np.testing.assert_array_equal(ta, tb)

@@ -30,9 +30,10 @@ ref = m.run_adam(g, nsteps=N, learning_rate=1e-3, use_engine=False)
 scratch = torch.zeros(1, device=dev)
 
 
-def run(schedule, sync, user=None):
+def run(schedule, sync, user=None, replay=True):
     eng = GraphAdamEngine(m, graph=True)
     eng.setup(g, nsteps=N, learning_rate=1e-3)
+    eng.step_replay = replay
     for mode in schedule:
         eng.use_graph = mode == "g"
         eng.step()
@@ -56,6 +57,11 @@ for sched in ("eeeeeggggggggggggggg", "eeeeeggggggeeeeegggg", "eeeeeggggggeeeeee
         for user in (None, "engine_stream"):
             print(sched, "sync" if sync else "nosync", user or "-", run(sched, sync, user),
                   flush=True)
-print("-- not protected (user kernels on the default stream between direct step() calls):")
+print("-- user kernels on the default stream between direct step() calls:")
 for sched in ("eeeeeggggggeeeeegggg", "gggggggggggggggggggg"):
-    print(sched, "sync default_stream", run(sched, True, "default_stream"), flush=True)
+    # default (round 5): direct step() calls launch eagerly -> exact
+    print(sched, "sync default_stream", run(sched, True, "default_stream", replay=False),
+          flush=True)
+    # opting in to replays of direct calls (step_replay) exposes the runtime defect
+    print(sched, "sync default_stream step_replay", run(sched, True, "default_stream"),
+          flush=True)
