@@ -67,6 +67,13 @@ def _args(argv=None):
                     help="fraction of populations (scattered by a hash) with a narrow true "
                          "sigma (bin width > 0.5 sigma: outside the Euler-Maclaurin forward's "
                          "range, evaluated by the per-edge path); the headline is 0")
+    ap.add_argument("--narrow-guess", type=float, default=None,
+                    help="starting log10 sigma of the narrow populations (default: truth + 0.1); "
+                         "a wide start (e.g. -0.6) makes the fit cross the Euler-Maclaurin limit "
+                         "mid-run (the engine re-lays the lanes out)")
+    ap.add_argument("--phase-steps", type=int, default=0,
+                    help="also report the step rate of every window of this many timed steps "
+                         "(a host sync per window)")
     ap.add_argument("--bounds", default="none", choices=["none", "both", "mixed"],
                     help="box constraints (reference run_adam(param_bounds=...)): 'both' boxes "
                          "every parameter around the start (truth inside), 'mixed' gives the "
@@ -152,7 +159,8 @@ def time_placement(placement, args, comm, dev, sync):
                                 placement=placement if comm.size > 1 else "hashed",
                                 layout=args.layout,
                                 lane_order=None if args.lane_order == "auto" else args.lane_order,
-                                narrow_frac=args.narrow_frac)
+                                narrow_frac=args.narrow_frac,
+                                narrow_guess_log_sigma=args.narrow_guess)
     model = PopulationSMFModel(aux_data=data, comm=comm)
     model.set_target_from_truth()
     history = args.history if args.history in ("full", "last") else int(args.history)
@@ -175,7 +183,23 @@ def time_placement(placement, args, comm, dev, sync):
     comm.barrier()
     sync()
     t0 = time.perf_counter()
-    engine.steps(args.steps)  # graph mode: blocks of engine.graph_steps steps per replay
+    phases = []
+    if args.phase_steps > 0:
+        done = 0
+        while done < args.steps:
+            w = min(args.phase_steps, args.steps - done)
+            tw = time.perf_counter()
+            nrel = len(getattr(engine, "relayouts", []))
+            engine.steps(w)
+            sync()
+            phases.append({"first_step": done, "steps": w,
+                           "ms_per_step": round(1e3 * (time.perf_counter() - tw) / w, 4),
+                           "relayouts": len(getattr(engine, "relayouts", [])) - nrel,
+                           "per_edge_share": round(model.engine_layout_share(
+                               comm.rank if engine.owner else None), 4)})
+            done += w
+    else:
+        engine.steps(args.steps)  # graph mode: blocks of engine.graph_steps steps per replay
     engine.drain()  # the pipelined last update / last all-gathers are inside the timing
     sync()
     comm.barrier()
@@ -216,6 +240,8 @@ def time_placement(placement, args, comm, dev, sync):
         "history": history,
         "device_ops_per_step": ops or None,
         "autotune": getattr(engine, "tuning", None),
+        "relayouts": list(getattr(engine, "relayouts", [])),
+        "phases": phases or None,
     }
     if args.profile_phases:
         info["phases_ms"] = {k: round(v, 4) for k, v in engine.timer.summary().items()}
@@ -322,6 +348,8 @@ def main(argv=None):
             "layout": head["layout"],
             "narrow_frac": args.narrow_frac,
             "bounds": args.bounds,
+            "narrow_guess": args.narrow_guess,
+            "relayouts": head["relayouts"],
             "per_edge_groups": head["fallback_groups"],
             "device_ops_per_step": head["device_ops_per_step"],
             "autotune": head["autotune"],
@@ -332,6 +360,8 @@ def main(argv=None):
         "loss_last": head["loss_last"],
         "setup_s": head["setup_s"],
     }
+    if head["phases"]:
+        rec["phases"] = head["phases"]
     if comm.size > 1:
         # connect-time verdicts of the peer-memory collectives: stress self-test passed
         # (back-to-back device-only exchanges) or the RCCL fallback and why

@@ -328,6 +328,7 @@ class FusedAdamEngine:
         if hint is not None:  # e.g. lanes grouped by forward path at the starting point
             hint(guess)
         md.engine_set_chunks(ub)
+        self._ub = list(ub)
         if self.size > 1 and dev.type == "cuda" and self.fuse_epilogue:
             from ..parallel.xgmi import get_oneshot
             self.oneshot = get_oneshot(self.comm)  # collective (all ranks run setup)
@@ -335,15 +336,7 @@ class FusedAdamEngine:
         # (e.g. the lanes layout's slot order, for coalesced parameter/gradient access).
         # It must keep every chunk's units inside the chunk, and be the same on all ranks;
         # user-facing values (guess, bounds, params, trajectory) are permuted at the edge.
-        perm = getattr(md, "engine_param_perm", lambda: None)()
-        if perm is not None:
-            perm = torch.as_tensor(perm, device=dev).to(torch.int64)
-            ar = torch.arange(upp, device=dev, dtype=torch.int64)
-            self.pidx = (perm[:, None] * upp + ar).reshape(-1)     # internal -> user index
-            self.inv_pidx = torch.empty_like(self.pidx)
-            self.inv_pidx[self.pidx] = torch.arange(P, device=dev)  # user -> internal index
-        else:
-            self.pidx = self.inv_pidx = None
+        self.pidx, self.inv_pidx = self._param_order(md, P, upp, dev)
         self.P, self.P_pad, self.pb, self.lengths = P, P_pad, pb, lengths
         self.C = len(lengths)
         self.lr, self.b1, self.b2, self.eps = float(learning_rate), float(b1), float(b2), float(eps)
@@ -509,6 +502,7 @@ class FusedAdamEngine:
         self.graph = None
         self.tuning = None
         self._tuning = False
+        self._relayout_init()
         self.ready = True
         if self.size > 1 and dev.type == "cuda":
             # line the ranks up before the first peer-memory exchange: a kernel waits for
@@ -538,6 +532,174 @@ class FusedAdamEngine:
             self._autotune(cands, min_window_s=1e-3 * float(
                 os.environ.get("MULTIGRAD_AUTOTUNE_WINDOW_MS", "30")))
         return self
+
+    @staticmethod
+    def _param_order(md, P: int, upp: int, dev):
+        """``(pidx, inv_pidx)``: internal -> user and user -> internal parameter index of
+        the model's unit order (``engine_param_perm``), or ``(None, None)``."""
+        perm = getattr(md, "engine_param_perm", lambda: None)()
+        if perm is None:
+            return None, None
+        perm = torch.as_tensor(perm, device=dev).to(torch.int64)
+        ar = torch.arange(upp, device=dev, dtype=torch.int64)
+        pidx = (perm[:, None] * upp + ar).reshape(-1)      # internal -> user index
+        inv = torch.empty_like(pidx)
+        inv[pidx] = torch.arange(P, device=dev)            # user -> internal index
+        return pidx, inv
+
+    # ------------------------------------------------------------------ re-layout
+    # A fit can move populations across the Euler-Maclaurin limit (the reference's own SMF
+    # fit takes sigma from 0.5 to 0.2 dex on 0.1-dex bins, tests/smf_example/
+    # smf_grad_descent.py:103,113): the lane classes laid out at setup then no longer
+    # match, narrow populations sit scattered in wide groups and most groups take the
+    # per-edge path (1% scattered narrow populations: ~47% of the groups).  Every
+    # MULTIGRAD_RELAYOUT_EVERY (16) steps the engine measures on the device, without a host sync,
+    # the share of groups the forward at the current parameters sends down the per-edge
+    # path (model.engine_relayout_probe), reads it back a few steps later, and when it
+    # differs from the share the classes were laid out for by more than
+    # MULTIGRAD_RELAYOUT_MARGIN it re-classifies at the step boundary: the lanes are rebuilt
+    # on the GPU (ops/_schedule.py:build_lanes_torch, ms) and theta / m / v / u / bounds are
+    # permuted into the new internal order.  Trajectory rows keep the order they were
+    # written in; each row range is mapped back to the user order with its own permutation.
+    def _relayout_init(self) -> None:
+        md = self.model
+        every = int(os.environ.get("MULTIGRAD_RELAYOUT_EVERY", "16") or 0)
+        self.relayout_every = every
+        self.relayout_margin = float(os.environ.get("MULTIGRAD_RELAYOUT_MARGIN", "0.02"))
+        self._relayout_on = bool(
+            every > 0 and _env_flag("MULTIGRAD_RELAYOUT", True) and self.device.type == "cuda"
+            and (self.size == 1 or self.owner) and self.pidx is not None
+            and hasattr(md, "engine_relayout_probe") and hasattr(md, "engine_layout_share"))
+        self._probe_step = None
+        self._probe_last = 0
+        self._probe_host = None
+        self._probe_ev = None
+        self._share_ref = self._probe_now() if self._relayout_on else None
+        self.relayouts: List[dict] = []
+        # trajectory row ranges and the user -> internal map they were written with
+        self._segs = [(0, self.inv_pidx)]
+
+    def _probe_now(self) -> Optional[float]:
+        """The probe's per-edge share at the current parameters (host sync)."""
+        v = self.model.engine_relayout_probe(self.theta, self.rank if self.owner else None)
+        return None if v is None else float(v)
+
+    def _maybe_relayout(self) -> None:
+        """Step-boundary hook: launch the device probe every ``relayout_every`` steps and act
+        on its value ``_PROBE_DELAY`` steps later (deterministic step: owner ranks vote)."""
+        if not getattr(self, "_relayout_on", False) or self._tuning or self._capturing:
+            return
+        k = self.step_host
+        if self._probe_step is None:
+            if k - self._probe_last < self.relayout_every:
+                return
+            v = self.model.engine_relayout_probe(self.theta, self.rank if self.owner else None)
+            if v is None:
+                self._relayout_on = False
+                return
+            if self._probe_host is None:
+                self._probe_host = torch.zeros(1, dtype=torch.float32, pin_memory=True)
+                self._probe_ev = torch.cuda.Event()
+            self._probe_host.copy_(v.reshape(1), non_blocking=True)
+            self._probe_ev.record()
+            self._probe_step = k
+            return
+        if k - self._probe_step < self._PROBE_DELAY:
+            return
+        self._probe_ev.synchronize()  # recorded _PROBE_DELAY steps ago: normally long done
+        f_cur = float(self._probe_host[0])
+        self._probe_step, self._probe_last = None, k
+        # the probe's share right after the last (re)layout is the reference: a drift by
+        # more than the margin either way means populations crossed the limit since
+        f_ref = self._share_ref if self._share_ref is not None else 0.0
+        go = abs(f_cur - f_ref) > self.relayout_margin
+        if self.owner and self.size > 1:
+            flag = torch.tensor([1 if go else 0], dtype=torch.int64)
+            self.comm.all_reduce(flag, op="max")
+            go = bool(flag[0])
+        if go and not self.relayout(reason=dict(step=k, share_probe=round(f_cur, 4),
+                                                share_ref=round(f_ref, 4))):
+            self._share_ref = f_cur  # classes unchanged: nothing to gain, stop re-trying
+
+    _PROBE_DELAY = 4
+
+    @on_engine_stream
+    def relayout(self, reason: Optional[dict] = None) -> bool:
+        """Re-classify the lane groups at the current parameters and rebuild the layout
+        (collective in owner mode).  Returns whether the classes changed."""
+        md = self.model
+        if self.pidx is None or not hasattr(md, "engine_layout_hint"):
+            return False
+        t0 = time.perf_counter()
+        self.drain()
+        P, dev = self.P, self.device
+        if self.owner:
+            a, b = self.own_range
+            full = self._assemble(self.theta[a:b])
+        else:
+            full = self.theta[:P]
+        band = float(os.environ.get("MULTIGRAD_RELAYOUT_BAND", "0.02"))
+        if not md.engine_layout_hint(self.to_user(full), band=band):
+            return False
+        old_inv = self.inv_pidx
+        md.engine_set_chunks(self._ub)
+        pidx, inv = self._param_order(md, P, self.upp, dev)
+        g = old_inv[pidx]  # new internal position i holds old internal position g[i]
+        if self.owner:
+            a, b = self.own_range
+            loc = g[a:b] - a
+            self.theta[a:b] = self.theta[g[a:b]]
+            for name in ("m", "v", "u_loc"):
+                t = getattr(self, name, None)
+                if t is not None:
+                    t.copy_(t[loc])
+            if self.bounds_loc is not None:
+                bl = self.bounds_loc
+                self.bounds_loc = Bounds(bl.lo[loc].contiguous(), bl.hi[loc].contiguous(),
+                                         bl.kind[loc].contiguous())
+        else:
+            self.theta[:P] = self.theta[:P][g]
+            for name in ("m", "v"):
+                t = getattr(self, name)
+                t[:P] = t[:P][g]
+            if self.bounds is not None:
+                self.u[:P] = self.u[:P][g]
+        if self.bounds is not None:
+            bd = self.bounds
+            pad = torch.arange(P, bd.lo.numel(), device=dev)
+            gi = torch.cat([g, pad])
+            self.bounds = Bounds(bd.lo[gi].contiguous(), bd.hi[gi].contiguous(),
+                                 bd.kind[gi].contiguous())
+        if self.history.mode != "full":
+            self.history.rows = [r[g] for r in self.history.rows]
+        self.pidx, self.inv_pidx = pidx, inv
+        self._segs.append((self.step_host + 1, inv))
+        rows = [md.engine_fwd_rows(c) for c in range(self.C)]
+        if sum(rows) * self.nS > self.slab.numel():
+            self.slab = torch.zeros(sum(rows) * self.nS, dtype=torch.float32, device=dev)
+        self.rows = rows
+        self.graph = None  # captured with the old layout's buffers
+        torch.cuda.synchronize()
+        self._share_ref = self._probe_now()
+        rec = dict(reason or {}, step=self.step_host, seconds=round(time.perf_counter() - t0, 4),
+                   share_new=round(self._share_ref, 4) if self._share_ref is not None else None,
+                   share_layout=round(md.engine_layout_share(self.rank if self.owner else None), 4))
+        self.relayouts.append(rec)
+        return True
+
+    def _traj_to_user(self, t: torch.Tensor) -> torch.Tensor:
+        """Trajectory rows (internal order of the layout they were written in) -> user order."""
+        segs = getattr(self, "_segs", None)
+        if self.pidx is None or not segs or len(segs) == 1:
+            return self.to_user(t)
+        out = torch.empty_like(t)
+        n = t.shape[0]
+        for i, (r0, inv) in enumerate(segs):
+            r1 = segs[i + 1][0] if i + 1 < len(segs) else n
+            r0, r1 = min(r0, n), min(r1, n)
+            if r1 > r0:
+                out[r0:r1] = t[r0:r1][..., inv]
+        return out
 
     # ------------------------------------------------------------------ setup-time tuning
     def _tl(self):
@@ -1186,6 +1348,7 @@ class FusedAdamEngine:
             else:
                 self._raw_step()
                 n -= 1
+            self._maybe_relayout()
 
     @on_engine_stream
     def steps(self, n: int):
@@ -1227,6 +1390,11 @@ class FusedAdamEngine:
         if self.step_host >= self.nsteps and self.history.mode == "full":
             raise RuntimeError("more steps than the trajectory buffer was sized for")
         self._raw_step(replay)
+        self._record_history()
+        self._maybe_relayout()
+
+    def _record_history(self) -> None:
+        """Host-side trajectory bookkeeping after a step (history "last" / stride)."""
         if self.history.mode != "full" and self.traj_loc is None:
             if self.pipeline:
                 st = self.history.stride
@@ -1254,10 +1422,12 @@ class FusedAdamEngine:
         self.drain()
         self.check("trajectory", collective=True)
         if self.traj_loc is None:
+            if self.history.mode == "full":
+                return self._traj_to_user(self.history.result())
             return self.to_user(self.history.result())
         if self.owner:
             rows = self.step_host + 1
-            return self.to_user(self._assemble(self.traj_loc[:rows].contiguous()))
+            return self._traj_to_user(self._assemble(self.traj_loc[:rows].contiguous()))
         W = self.size
         nloc = self.traj_loc.shape[1]
         rows = self.step_host + 1
@@ -1383,12 +1553,41 @@ class FusedAdamEngine:
               "u": None if u is None else u.detach().cpu().clone()}
         rows = self.step_host + 1
         if self.traj_loc is not None:
-            st["traj"] = self.traj_loc[:rows].detach().cpu().clone()
+            st["traj"] = self._traj_rows_to_current(self.traj_loc[:rows]).detach().cpu().clone()
         elif self.history.mode == "full":
-            st["traj"] = self.history.buf[:rows].detach().cpu().clone()
+            st["traj"] = self._traj_rows_to_current(self.history.buf[:rows]).detach().cpu().clone()
         else:
             st["history_rows"] = [r.detach().cpu().clone() for r in self.history.rows]
+        if self.pidx is not None:
+            # the user parameter index of every local element: a checkpoint written after a
+            # re-layout loads into an engine laid out differently (e.g. at the guess)
+            st["units_order"] = self._local_order().cpu().clone()
+            if self.history.mode != "full" and self.traj_loc is None:
+                st["units_order_full"] = self.pidx.cpu().clone()
         return st
+
+    def _local_order(self) -> torch.Tensor:
+        """User parameter index of each element of this rank's optimizer vectors."""
+        if self.owner:
+            a, b = self.own_range
+            return self.pidx[a:b]
+        return self.pidx
+
+    def _traj_rows_to_current(self, t: torch.Tensor) -> torch.Tensor:
+        """Trajectory rows (each in the layout it was written in) -> the current internal
+        order (columns: this rank's local elements)."""
+        segs = getattr(self, "_segs", None)
+        if self.pidx is None or not segs or len(segs) == 1:
+            return t
+        base = self.own_range[0] if self.owner else 0
+        cur = self._local_order()
+        out = t.clone()
+        n = t.shape[0]
+        for i, (r0, inv) in enumerate(segs[:-1]):
+            r1 = min(segs[i + 1][0], n)
+            if r1 > min(r0, n):
+                out[r0:r1, :cur.numel()] = t[r0:r1][:, inv[cur] - base]
+        return out
 
     @on_engine_stream
     def load_state_dict(self, st: dict) -> int:
@@ -1435,10 +1634,45 @@ class FusedAdamEngine:
             dst[:tr.shape[0]].copy_(tr)
         elif "history_rows" in st:
             self.history.rows = [r.to(dev) for r in st["history_rows"]]
+        if st.get("units_order") is not None and self.pidx is not None:
+            full = st.get("units_order_full")
+            self._reorder_loaded(st["units_order"].to(dev), None if full is None else full.to(dev))
+        self._segs = [(0, self.inv_pidx)]
         self.step_host = step
         self.step_dev[:, 0] = step
         self.step_dev[:, 1] = 0
         return step
+
+    def _reorder_loaded(self, saved: torch.Tensor, saved_full: Optional[torch.Tensor]) -> None:
+        """Permute freshly loaded vectors from the checkpoint's internal order (``saved``:
+        user index per local element; ``saved_full``: per element of the full vector) into
+        this engine's."""
+        def positions(order):
+            pos = torch.empty(self.P, dtype=torch.int64, device=order.device)
+            pos[order] = torch.arange(order.numel(), device=order.device)
+            return pos
+
+        cur = self._local_order()
+        if not torch.equal(saved, cur):
+            idx = positions(saved)[cur]  # position of each current local element when saved
+            n = cur.numel()
+            if self.owner:
+                a, b = self.own_range
+                self.theta[a:b] = self.theta[a:b][idx]
+                vecs = [self.m, self.v] + ([self.u_loc] if self.u_loc is not None else [])
+            else:
+                self.theta[:n] = self.theta[:n][idx]
+                vecs = [self.m, self.v] + ([self.u] if self.bounds is not None else [])
+            for t in vecs:
+                t[:n] = t[:n][idx]
+            traj = self.traj_loc if self.traj_loc is not None else (
+                self.history.buf if self.history.mode == "full" else None)
+            if traj is not None:
+                traj[:, :n] = traj[:, :n][:, idx]
+        if saved_full is not None and self.history.mode != "full" and self.traj_loc is None \
+                and not torch.equal(saved_full, self.pidx):
+            idx = positions(saved_full)[self.pidx]
+            self.history.rows = [r[idx] for r in self.history.rows]
 
     @on_engine_stream
     def save_checkpoint(self, path: str) -> None:

@@ -91,7 +91,8 @@ def make_population_data(num_params: int = 10_000_000, num_halos: int = 1 << 27,
                          truth_offset=(0.1, 0.1), tail: str = "absolute",
                          layout: str = "auto", placement: str = "hashed",
                          lane_order: Optional[str] = None, narrow_frac: float = 0.0,
-                         narrow_log_sigma: float = -1.1) -> dict:
+                         narrow_log_sigma: float = -1.1,
+                         narrow_guess_log_sigma: Optional[float] = None) -> dict:
     """This rank's shard of the synthetic population-SMF data set.
 
     The global catalog (halo i: population ``hash(i) mod J``, log mass from a second hash)
@@ -124,7 +125,10 @@ def make_population_data(num_params: int = 10_000_000, num_halos: int = 1 << 27,
     scattered over the catalog) whose true log10 sigma is ``narrow_log_sigma`` (default
     -1.1: sigma = 0.079 dex, a bin width of 1.26 sigma at the truth and 1.0 sigma at the
     default guess), outside the Euler-Maclaurin forward's range of 0.5 sigma; these
-    populations take the per-edge path (profiles/narrow_sweep/).
+    populations take the per-edge path (profiles/narrow_sweep/).  ``narrow_guess_log_sigma``:
+    the starting log10 sigma of those populations (default: truth + offset, as the others);
+    a wide start (e.g. -0.6, inside the Euler-Maclaurin range) makes a fit move them across
+    the limit while it runs (the engine's re-layout, engine/fused.py).
 
     Returns a dict with the sorted device shard (``shard``), bins, volume, true
     parameters ``truth`` (interleaved, device) and a starting ``guess``; the target SMF is
@@ -169,6 +173,7 @@ def make_population_data(num_params: int = 10_000_000, num_halos: int = 1 << 27,
     truth = torch.empty(2 * npop, dtype=torch.float32, device=device)
     truth[0::2] = (-2.0 + 0.2 * (hash_uniform(cidx, seed + 2) - 0.5)).to(torch.float32)
     truth[1::2] = (-0.5 + 0.2 * (hash_uniform(cidx, seed + 3) - 0.5)).to(torch.float32)
+    narrow = None
     if narrow_frac > 0:
         narrow = hash_uniform(cidx, seed + 4) < float(narrow_frac)
         truth[1::2] = torch.where(narrow, torch.full_like(truth[1::2], float(narrow_log_sigma)),
@@ -176,6 +181,9 @@ def make_population_data(num_params: int = 10_000_000, num_halos: int = 1 << 27,
     guess = truth.clone()
     guess[0::2] += truth_offset[0]
     guess[1::2] += truth_offset[1]
+    if narrow is not None and narrow_guess_log_sigma is not None:
+        guess[1::2] = torch.where(narrow, torch.full_like(guess[1::2], float(narrow_guess_log_sigma)),
+                                  guess[1::2])
     edges = np.linspace(8.5, 9.5, nbins + 1)
     # volume normalises the SMF to O(1e-2) per bin like the reference's tests
     volume = 10.0 * num_halos
@@ -258,22 +266,51 @@ class PopulationSMFModel(OnePointModel):
         g = per_slot.reshape(-1, 64).amax(1)
         return int(g.sum()), int(g.numel())
 
-    def engine_layout_hint(self, guess) -> None:
-        """Group the lanes by forward path at the starting parameters (called by the fused
-        engine before :meth:`engine_set_chunks`): populations whose bin width exceeds the
-        Euler-Maclaurin range (h = delta / sigma > 0.5, csrc/smf.hip kEmHMax) get lane groups
-        of their own, so a few narrow populations do not send whole groups to the per-edge
-        path.  ``MULTIGRAD_LANE_CLASSES=0`` turns it off."""
+    def engine_layout_hint(self, guess, band: float = 0.0) -> bool:
+        """Group the lanes by forward path at ``guess`` (user-order parameters; called by the
+        fused engine before :meth:`engine_set_chunks`, at setup and when it re-lays the lanes
+        out during a fit): populations whose bin width exceeds the Euler-Maclaurin range
+        (h = delta / sigma > 0.5, csrc/smf.hip kEmHMax) get lane groups of their own, so a
+        few narrow populations do not send whole groups to the per-edge path.  Returns
+        whether the classes changed.  ``MULTIGRAD_LANE_CLASSES=0`` turns it off."""
         sh = self.shard
-        if sh.layout != "lanes" or os.environ.get("MULTIGRAD_LANE_CLASSES", "1") == "0":
-            return
+        if not self._lane_classes_apply():
+            return False
         d = self.bins.delta
-        if d <= 0 or self.bins.rel_tail:
-            return
         g = torch.as_tensor(guess).reshape(-1)
-        s = g[1::2].detach().to("cpu", torch.float64)
-        # h = delta / 10^s > 0.5  <=>  s < log10(2 delta)
-        sh.set_lane_classes((s < math.log10(2.0 * d)).to(torch.int64))
+        s = g[1::2].detach()
+        s = s.to(torch.float64) if s.is_cuda else s.to("cpu", torch.float64)
+        # h = delta / 10^s > 0.5  <=>  s < log10(2 delta); ``band`` (re-layouts during a fit)
+        # also groups the populations within band dex above the limit with the narrow ones,
+        # so a fit that moves them across it a little later needs no second re-layout
+        return sh.set_lane_classes((s < math.log10(2.0 * d) + band).to(torch.int64))
+
+    def _lane_classes_apply(self) -> bool:
+        sh = self.shard
+        return (sh.layout == "lanes" and os.environ.get("MULTIGRAD_LANE_CLASSES", "1") != "0"
+                and self.bins.delta > 0 and not self.bins.rel_tail)
+
+    def engine_relayout_probe(self, theta, chunk=None):
+        """Device scalar (no host sync): the share of the lane groups of ``chunk`` that the
+        forward at ``theta`` (engine internal order) sends down the per-edge path -- groups
+        with any lane outside the Euler-Maclaurin range.  The engine compares it with
+        :meth:`engine_layout_share` (the share the current lane classes were laid out for)
+        and re-lays the lanes out when a fit has moved populations across the limit.  None
+        when classes do not apply."""
+        sh = self.shard
+        if not self._lane_classes_apply() or sh.device.type != "cuda":
+            return None
+        g0, g1 = sh.group_range(chunk)
+        if g1 <= g0:
+            return torch.zeros((), device=theta.device)
+        sp = sh.slot_pidx[64 * g0:64 * g1].long()
+        s = theta.reshape(-1)[1:2 * self.aux_data["npop"]:2]
+        narrow = (sp >= 0) & (s[sp.clamp(min=0)] < math.log10(2.0 * self.bins.delta))
+        return narrow.view(-1, 64).any(1).float().mean()
+
+    def engine_layout_share(self, chunk=None) -> float:
+        """The per-edge group share the current lane classes imply (host)."""
+        return self.shard.per_edge_share(chunk)
 
     def engine_owner_units(self):
         """Population (unit) bounds ``[W+1]`` of the owner placement, or None."""

@@ -229,51 +229,77 @@ class PopulationShard:
                                     device=self.device)
 
     def set_lane_classes(self, cls: Optional[torch.Tensor]) -> bool:
-        """Per-population class (int, CPU or device, [npop]) that orders the slots of a
-        lanes window before the halo count: populations of one class share 64-lane groups.
-        The Euler-Maclaurin forward takes a group's fast path only when every lane's bin
-        width is inside its range, so the narrow populations of a fit (bin width > 0.5
+        """Per-population class (int, [npop], CPU or on the shard's device) that orders the
+        slots of a lanes window before the halo count: populations of one class share 64-lane
+        groups.  The Euler-Maclaurin forward takes a group's fast path only when every lane's
+        bin width is inside its range, so the narrow populations of a fit (bin width > 0.5
         sigma) are kept out of the other groups -- at 1% narrow populations in random
         places, 47% of the groups would otherwise hold one.  Takes effect at the next
         :meth:`set_chunks`; the class must be the same on every rank.  Returns whether it
-        changed."""
+        changed.  Kept on the shard's device when given there (the engine's re-layout
+        computes it on the GPU: no host round trip of 5e6-entry vectors)."""
         if cls is not None:
-            cls = torch.as_tensor(cls).reshape(-1).to("cpu", torch.int64)
+            cls = torch.as_tensor(cls).reshape(-1).to(torch.int64)
+            if cls.device != self.device and cls.device.type != "cpu":
+                cls = cls.to(self.device)
             assert cls.numel() == self.npop
             if not bool((cls != 0).any()):
                 cls = None
         old = self.lane_class
         self.lane_class = cls
-        return not ((old is None and cls is None) or
-                    (old is not None and cls is not None and torch.equal(old, cls)))
+        if old is None or cls is None:
+            return not (old is None and cls is None)
+        return not torch.equal(old.to(cls.device), cls)
 
-    def per_edge_share(self) -> float:
-        """Share of the lane groups that hold a population of lane class != 0 (the narrow
-        populations of :meth:`set_lane_classes`): the groups the residual forward evaluates
-        by per-edge tails.  Cached per layout."""
+    def per_edge_share(self, chunk: Optional[int] = None) -> float:
+        """Share of the lane groups (of ``chunk``, default all) that hold a population of
+        lane class != 0 (the narrow populations of :meth:`set_lane_classes`): the groups the
+        residual forward evaluates by per-edge tails.  Cached per layout."""
         if self.layout != "lanes" or self.lane_class is None or self.ngroups == 0:
             return 0.0
-        if getattr(self, "_pe_share", None) is None:
-            sp = self.slot_pop.to("cpu", torch.int64)
-            c = torch.where(sp >= 0, self.lane_class[sp.clamp(min=0)], torch.zeros(1, dtype=torch.int64))
-            self._pe_share = float((c.reshape(-1, 64).amax(1) > 0).double().mean())
-        return self._pe_share
+        cache = self.__dict__.setdefault("_pe_share", None)
+        if cache is None:
+            cls = self.lane_class
+            sp = self.slot_pop.to(cls.device, torch.int64)
+            c = torch.where(sp >= 0, cls[sp.clamp(min=0)], torch.zeros_like(sp))
+            per_group = (c.reshape(-1, 64).amax(1) > 0).double()
+            # cumulative counts: any chunk's share from one host copy
+            cum = torch.zeros(per_group.numel() + 1, dtype=torch.float64, device=per_group.device)
+            cum[1:] = torch.cumsum(per_group, 0)
+            cache = self._pe_share = cum.cpu()
+        g0, g1 = self.group_range(chunk)
+        return float((cache[g1] - cache[g0]) / (g1 - g0)) if g1 > g0 else 0.0
 
     def _order_key(self):
         key = self.order_counts
         if self.lane_class is None:
             return key
+        cls = self.lane_class
+        if cls.device.type != "cpu":
+            if getattr(self, "_key_base_dev", None) is None or self._key_base_dev.device != cls.device:
+                base = self.counts if key is None else key
+                self._key_base_dev = base.to(device=cls.device, dtype=torch.int64)
+            return self._key_base_dev + (cls << 40)
         base = self.counts.to(torch.int64) if key is None else key
-        return base + (self.lane_class << 40)
+        return base + (cls << 40)
 
     def _build_lanes(self, pb) -> None:
-        from ._schedule import build_lanes_py
+        from ._schedule import build_lanes_py, build_lanes_torch
         key = self._order_key()
-        try:
-            out = ext().build_lanes(self.counts.to(torch.int64), list(pb[1:-1]),
-                                    self._lane_window, self._lane_lmax, key)
-        except ImportError:
-            out = build_lanes_py(self.counts, pb[1:-1], self._lane_window, self._lane_lmax, key)
+        out = None
+        if self.device.type == "cuda" and os.environ.get("MULTIGRAD_LANES_BUILDER", "device") != "host":
+            # the same schedule from sorts and scatters on the GPU (~ms; the host builder takes
+            # ~1 s at 5e6 populations): what makes a re-layout during a fit affordable
+            if getattr(self, "_counts_dev", None) is None:
+                self._counts_dev = self.counts.to(self.device, torch.int64)
+            out = build_lanes_torch(self._counts_dev, pb[1:-1], self._lane_window,
+                                    self._lane_lmax, key, device=self.device)
+        if out is None:
+            try:
+                out = ext().build_lanes(self.counts.to(torch.int64), list(pb[1:-1]),
+                                        self._lane_window, self._lane_lmax, key)
+            except ImportError:
+                out = build_lanes_py(self.counts, pb[1:-1], self._lane_window, self._lane_lmax, key)
         (slot_pop, slot_src, slot_len, slot_part, group_base, group_len, chunk_groups, giant,
          chunk_giant, fwd_order, slot_pidx, perm) = out
         dev = self.device
@@ -585,7 +611,7 @@ def smf_forward_slab(theta: torch.Tensor, shard: PopulationShard, bins: SmfBins,
                                        shard.defer_buffer() if resid and lanes_fix_blocks()
                                        else shard.fold_ticket() if epilogue is not None else None,
                                        lanes_fix_blocks() if resid else 0, et, es, ep,
-                                       bool(resid and shard.per_edge_share() >= PER_EDGE_SHARE))
+                                       bool(resid and shard.per_edge_share(chunk) >= PER_EDGE_SHARE))
         if resid:
             shard.resid_epoch += 1
         return int(rows)

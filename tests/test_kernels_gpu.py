@@ -752,3 +752,60 @@ def test_narrow_populations_get_their_own_lane_groups():
     assert before[0] > 0.3 * before[1] and after[0] < 0.05 * after[1], (before, after)
     eng.steps(3)
     assert np.isfinite(eng.last_loss())
+
+
+def _crossing_model(seed=14, npar=6000, nhalo=300_000):
+    """20% of the populations start wide (log10 sigma -0.6, Euler-Maclaurin path) and fit
+    towards a narrow truth (-1.1): they cross the limit (-0.70) during the run."""
+    from multigrad_amd.models.population import PopulationSMFModel, make_population_data
+    data = make_population_data(num_params=npar, num_halos=nhalo, seed=seed, device=DEV,
+                                narrow_frac=0.2, narrow_guess_log_sigma=-0.6)
+    model = PopulationSMFModel(aux_data=data)
+    model.set_target_from_truth()
+    return model, data
+
+
+@pytest.mark.parametrize("owner,graph,history", [(False, False, "full"), (False, True, "full"),
+                                                 (True, False, "full"), (False, False, "last")])
+def test_relayout_during_fit_matches_static_layout(monkeypatch, owner, graph, history):
+    """populations crossing the Euler-Maclaurin limit mid-fit trigger a
+    re-layout (device probe -> re-classification -> lanes rebuilt on the GPU, theta / m / v
+    permuted); the trajectory equals the run that keeps its setup layout (rtol 1e-5)."""
+    from multigrad_amd.engine.fused import FusedAdamEngine
+    model, data = _crossing_model()
+    kw = dict(nsteps=40, learning_rate=2e-2, history=history)
+    monkeypatch.setenv("MULTIGRAD_RELAYOUT", "0")
+    ref_eng = FusedAdamEngine(model, graph=graph, owner=owner)
+    ref = ref_eng.run_adam(data["guess"], **kw)
+    assert not ref_eng.relayouts
+    monkeypatch.setenv("MULTIGRAD_RELAYOUT", "1")
+    monkeypatch.setenv("MULTIGRAD_RELAYOUT_EVERY", "4")
+    eng = FusedAdamEngine(model, graph=graph, owner=owner)
+    t = eng.run_adam(data["guess"], **kw)
+    assert eng.relayouts, "the crossing populations should have triggered a re-layout"
+    r = eng.relayouts[-1]
+    assert r["share_new"] < r["share_probe"]  # the narrow lanes are grouped again
+    torch.testing.assert_close(t, ref, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(eng.params(), ref[-1], rtol=1e-5, atol=1e-6)
+
+
+def test_relayout_checkpoint_resumes_in_setup_layout(tmp_path, monkeypatch):
+    """A checkpoint written after a re-layout resumes in an engine laid out at the guess
+    (the saved vectors carry their order) and continues the same trajectory."""
+    from multigrad_amd.engine.fused import FusedAdamEngine
+    model, data = _crossing_model(seed=15)
+    monkeypatch.setenv("MULTIGRAD_RELAYOUT_EVERY", "4")
+    a = FusedAdamEngine(model, graph=False)
+    a.setup(data["guess"], nsteps=30, learning_rate=2e-2)
+    a.steps(20)
+    assert a.relayouts
+    path = str(tmp_path / "ck.pt")
+    a.save_checkpoint(path)
+    a.steps(10)
+    ta = a.trajectory()
+    monkeypatch.setenv("MULTIGRAD_RELAYOUT", "0")
+    b = FusedAdamEngine(model, graph=False)
+    b.setup(data["guess"], nsteps=30, learning_rate=2e-2)
+    assert b.load_checkpoint(path) == 20
+    b.steps(10)
+    torch.testing.assert_close(b.trajectory(), ta, rtol=1e-5, atol=1e-6)

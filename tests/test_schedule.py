@@ -145,3 +145,27 @@ def test_lane_classes_group_narrow_populations():
     assert sh.set_lane_classes(None)
     sh.set_chunks(sh.chunk_pops)
     assert mixed_and_narrow()[0] == n0
+
+
+@pytest.mark.parametrize("J,breaks,window", [(5000, [], 4096), (20000, [7000, 13001], 4096),
+                                             (3000, [1000], 256), (130, [], 64), (1, [], 64)])
+def test_lanes_schedule_torch_builder_matches_native(J, breaks, window):
+    """The sort-and-scatter lanes builder (run on the GPU for re-layouts during a fit) gives
+    exactly the host builder's schedule: slots, groups, forward order, internal order."""
+    from multigrad_amd.ops._ext import ext
+    from multigrad_amd.ops._schedule import build_lanes_py, build_lanes_torch
+    g = torch.Generator().manual_seed(J)
+    cnt = torch.randint(0, 60, (J,), generator=g)
+    cls = (torch.rand(J, generator=g) < 0.05).long()
+    for key in (None, cnt + (cls << 40), cnt * 3 + 1):
+        try:
+            ref = ext().build_lanes(cnt.long(), breaks, window, 4096, key)
+        except ImportError:
+            ref = build_lanes_py(cnt, breaks, window, 4096, key)
+        got = build_lanes_torch(cnt, breaks, window, 4096, key)
+        assert got is not None
+        for a, b in zip(ref, got):
+            assert torch.equal(a.cpu().to(b.dtype), b.cpu())
+    big = cnt.clone()
+    big[0] = 5000  # a split population: the host builder's job
+    assert build_lanes_torch(big, breaks, window, 4096) is None
