@@ -6,7 +6,7 @@ set -o pipefail
 O=gpurun_out/r5_relayout
 mkdir -p $O
 export MULTIGRAD_PROGRESS=0
-true || timeout -k 10 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread \
+timeout -k 10 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread \
   "tests/test_kernels_gpu.py::test_relayout_during_fit_matches_static_layout" \
   "tests/test_kernels_gpu.py::test_relayout_checkpoint_resumes_in_setup_layout" \
   "tests/test_kernels_gpu.py::test_narrow_populations_get_their_own_lane_groups" \
