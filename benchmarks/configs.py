@@ -56,17 +56,18 @@ def adam(comm, steps, params, halos, history):
     m.set_target_from_truth()
     eng = m.fused_engine()
     eng.setup(data["guess"], nsteps=steps + 3, learning_rate=1e-3, history=history)
-    for _ in range(3):
-        eng.step()
+    eng.steps(3)
+    eng.drain()
     _sync(); comm.barrier(); _sync()
     t0 = time.perf_counter()
-    for _ in range(steps):
-        eng.step()
+    eng.steps(steps)
+    eng.drain()
     _sync(); comm.barrier()
     dt = time.perf_counter() - t0
     return {"config": f"adam-{params:.0e}param", "value": steps / dt, "unit": "steps/s",
-            "n_ranks": comm.size, "halos": halos, "zero": eng.zero, "chunks": eng.C,
-            "loss": eng.last_loss()}
+            "ms_per_step": 1e3 * dt / steps, "n_ranks": comm.size, "halos": halos,
+            "history": history, "zero": eng.zero, "chunks": eng.C, "pipelined": eng.pipeline,
+            "graph": bool(eng.use_graph), "loss": eng.last_loss()}
 
 
 def lbfgs(comm, iters, params, halos):
