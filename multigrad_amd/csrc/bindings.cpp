@@ -26,7 +26,6 @@ void smf_vjp(torch::Tensor x, c10::optional<torch::Tensor> pop, torch::Tensor th
              torch::Tensor grad, torch::Tensor partials, torch::Tensor giant,
              std::string exchange);
 int64_t smf_fwd_lanes_max_blocks(int64_t nb, bool log_sigma, bool rel_tail, bool resid);
-int64_t smf_lanes_fallback_mode();
 void smf_lanes_pack(torch::Tensor xs, torch::Tensor slot_src, torch::Tensor slot_len,
                     torch::Tensor group_base, torch::Tensor group_len, torch::Tensor xi);
 int64_t smf_forward_lanes(torch::Tensor xi, torch::Tensor slot_pop, torch::Tensor group_base,
@@ -40,7 +39,6 @@ int64_t smf_forward_lanes(torch::Tensor xi, torch::Tensor slot_pop, torch::Tenso
                        c10::optional<torch::Tensor> queues,
                        c10::optional<std::vector<torch::Tensor>> update,
                        std::vector<double> update_scalars,
-                       c10::optional<torch::Tensor> defer, int64_t fix_blocks,
                        std::vector<torch::Tensor> epi_tensors, std::vector<double> epi_scalars,
                        std::vector<int64_t> epi_peers, bool per_edge);
 void smf_vjp_lanes(torch::Tensor slot_pop, torch::Tensor slot_part, torch::Tensor theta,
@@ -152,7 +150,6 @@ PYBIND11_MODULE(_C, m) {
         pybind11::arg("giant"), pybind11::arg("exchange") = std::string());
   m.def("smf_fwd_lanes_max_blocks", &mg::smf_fwd_lanes_max_blocks);
   m.def("smf_lanes_pack", &mg::smf_lanes_pack);
-  m.def("smf_lanes_fallback_mode", &mg::smf_lanes_fallback_mode);
   m.def("smf_forward_lanes", &mg::smf_forward_lanes, pybind11::arg("xi"), pybind11::arg("slot_pop"),
         pybind11::arg("group_base"), pybind11::arg("group_len"), pybind11::arg("fwd_order"),
         pybind11::arg("theta"), pybind11::arg("edges"), pybind11::arg("scale"),
@@ -161,7 +158,6 @@ PYBIND11_MODULE(_C, m) {
         pybind11::arg("wave_order") = pybind11::none(), pybind11::arg("wave_start") = pybind11::none(),
         pybind11::arg("queues") = pybind11::none(), pybind11::arg("update") = pybind11::none(),
         pybind11::arg("update_scalars") = std::vector<double>(),
-        pybind11::arg("defer") = pybind11::none(), pybind11::arg("fix_blocks") = 0,
         pybind11::arg("epi_tensors") = std::vector<torch::Tensor>(),
         pybind11::arg("epi_scalars") = std::vector<double>(),
         pybind11::arg("epi_peers") = std::vector<int64_t>(), pybind11::arg("per_edge") = false);

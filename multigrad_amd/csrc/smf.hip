@@ -33,9 +33,6 @@
 
 namespace mg {
 
-#ifndef MG_FWD_BALLOT
-#define MG_FWD_BALLOT 1  // integer counts per wave (SALU) instead of per lane (VALU)
-#endif
 constexpr int kMaxBins = 32;
 constexpr int kXcds = 8;  // MI355X: 8 XCDs (L2 domains), workgroups dispatched round-robin
 constexpr int kThreads = 256;
@@ -76,7 +73,7 @@ __device__ __forceinline__ float inv_sigma(float s) {
   return LOGSIG ? fast_exp2(-s * kLog2_10) : 1.0f / s;
 }
 
-// Table path of the absolute contract (MG_FWD_TAB): the signed tail V(n) = sign(n) Q(|n|)
+// Table path of the absolute contract: the signed tail V(n) = sign(n) Q(|n|)
 // is read from a piecewise-cubic table (tail_table.h, tools/fit_tail_table.py: 96 pieces
 // over |z| <= 6, float32 chain error 8.8e-8 against 1.6e-7 for the rational polynomial)
 // held in LDS, instead of v_rcp + a degree-5 Horner chain + the product with exp2(-w^2):
@@ -87,17 +84,14 @@ __device__ __forceinline__ float inv_sigma(float s) {
 // LDS layout: REPL replicas of every entry, lane l reading replica l % REPL, so the 16
 // lanes of a ds_read_b128 lane group hit distinct bank quads (REPL = 16: conflict free;
 // 8: two lanes per replica).
-// MG_FWD_TAB = 1 (default): forwards WITHOUT residuals use the table -- there it also
-// removes the v_exp, and the lanes forward measured 440 vs 536-540 us at 1.34e8 halos.
-// MG_FWD_TAB = 2 also uses it in the residual forwards, where the exponential stays (for
-// G, W): measured slower there (pipelined 702 vs 628 us, residual 620 vs 570 us).  The
+// Forwards WITHOUT residuals use the table -- there it also removes the v_exp, and the
+// lanes forward measured 440 vs 536-540 us at 1.34e8 halos.  Using it in the residual
+// forwards too, where the exponential stays (for G, W), measured slower (pipelined 702 vs
+// 628 us, residual 620 vs 570 us; the switch was removed in round 5).  The
 // index arithmetic (v_med3, v_cvt_flr, v_fract, v_lshl_or: 4.2-4.3 cycles per wave each,
 // tools/ubench/op_rates.hip, against 2.7 for v_fma) eats most of what the v_rcp and the
 // Horner chain cost, and at 119-128 VGPRs the compiler waits for each table read right
 // after issuing it (docs/design.md, forward floor).
-#ifndef MG_FWD_TAB
-#define MG_FWD_TAB 1
-#endif
 __device__ __forceinline__ int cvt_flr_i32(float t) {
   int k;
   asm("v_cvt_flr_i32_f32 %0, %1" : "=v"(k) : "v"(t));
@@ -130,52 +124,20 @@ __device__ __forceinline__ const float4* tail_tab_lane(const float4* tab) {
 // counts; the per-bin differences are formed once per thread at the end.
 // A halo with x = -inf contributes exactly zero (used to mask the unrolled tail): every
 // V_e is -0 and every pos_e is 1, which cancels in the differences.
-#ifndef MG_FWD_TAB_FOLD
-#define MG_FWD_TAB_FOLD 1
-#endif
-#ifndef MG_FWD_TAB_BATCH
-#define MG_FWD_TAB_BATCH 1
-#endif
 template <int NB, bool LOGSIG, bool REL, int REPL = 0>
 __device__ __forceinline__ void halo_mass(float x, float2 th, const SmfBins& b,
                                           float (&acc)[NB + 1], int (&cnt)[NB + 1],
                                           const float4* __restrict__ tb = nullptr) {
   // table path: the coordinate is formed directly in table units (the piece scale folded
   // into the two per-halo factors: one multiply per halo instead of one per edge)
-  constexpr bool kFold = REPL > 0 && MG_FWD_TAB_FOLD;
+  constexpr bool kFold = REPL > 0;
   const float ninv = -inv_sigma<LOGSIG>(th.y) * (kFold ? kWScale * kTailTabInvH : kWScale);
   const float mu = -(x + th.x) * ninv;  // = (x + a) * kWScale / sigma (x kTailTabInvH)
-  if constexpr (kFold && MG_FWD_TAB_BATCH > 1) {
-    // table reads of MG_FWD_TAB_BATCH edges issued before their cubics (fewer LDS waits)
-    constexpr int BT = MG_FWD_TAB_BATCH;
-#pragma unroll
-    for (int e0 = 0; e0 <= NB; e0 += BT) {
-      float4 c[BT];
-      float s[BT];
-#pragma unroll
-      for (int j = 0; j < BT; ++j) {
-        const int e = e0 + j;
-        if (e > NB) break;
-        const float t = __builtin_amdgcn_fmed3f(fmaf(b.edge[e], ninv, mu), -(float)(kTailTabN / 2),
-                                                (float)(kTailTabN / 2) - 1.0f / 4096);
-        c[j] = tb[cvt_flr_i32(t) * REPL];
-        s[j] = __builtin_amdgcn_fractf(t);
-        cnt[e] += __builtin_popcountll(__builtin_amdgcn_ballot_w64(t < 0.0f));
-      }
-#pragma unroll
-      for (int j = 0; j < BT; ++j) {
-        const int e = e0 + j;
-        if (e > NB) break;
-        acc[e] += fma_scalar(fma_scalar(fma_scalar(c[j].w, s[j], c[j].z), s[j], c[j].y), s[j], c[j].x);
-      }
-    }
-    return;
-  }
 #pragma unroll
   for (int e = 0; e <= NB; ++e) {
     const float n = fmaf(b.edge[e], ninv, mu);
     if constexpr (REPL > 0) {  // signed-tail table (see ep_eval_tab)
-      const float t = __builtin_amdgcn_fmed3f(kFold ? n : n * kTailTabInvH, -(float)(kTailTabN / 2),
+      const float t = __builtin_amdgcn_fmed3f(n, -(float)(kTailTabN / 2),
                                               (float)(kTailTabN / 2) - 1.0f / 4096);
       const float4 c = tb[cvt_flr_i32(t) * REPL];
       const float s = __builtin_amdgcn_fractf(t);
@@ -186,12 +148,8 @@ __device__ __forceinline__ void halo_mass(float x, float2 th, const SmfBins& b,
     float p, g;
     normal_tail_parts_w<REL>(n, p, g);
     acc[e] = fmaf(p, __builtin_copysignf(g, n), acc[e]);
-#if MG_FWD_BALLOT
     // wave-wide count of the 0/1 parts: one v_cmp, the popcount/add run on the SALU
     cnt[e] += __builtin_popcountll(__builtin_amdgcn_ballot_w64(n < 0.0f));
-#else
-    cnt[e] += (int)(__float_as_uint(n) >> 31);
-#endif
   }
 }
 
@@ -203,9 +161,6 @@ __device__ __forceinline__ void halo_mass(float x, float2 th, const SmfBins& b,
 #define MG_FWD_MINWAVES 8
 #endif
 constexpr int kFwdUnroll = MG_FWD_UNROLL;
-#ifndef MG_FWD_PIPE
-#define MG_FWD_PIPE 1
-#endif
 
 // XS (fused exchange): workgroups [0, xs.blocks) run the two-shot exchange of the previous
 // parameter chunk (twoshot.h) and the rest this forward, with their own block numbering --
@@ -226,7 +181,7 @@ __global__ __launch_bounds__(kThreads, MG_FWD_MINWAVES) void smf_fwd_kernel(
     nblk -= xs.blocks;
   }
   // signed-tail table: 8 replicas (8 workgroups per CU share the LDS)
-  constexpr int kRepl = (!REL && MG_FWD_TAB >= 1 && MG_FWD_BALLOT) ? 8 : 0;
+  constexpr int kRepl = !REL ? 8 : 0;
   const float4* tb = nullptr;
   if constexpr (kRepl > 0) {
     __shared__ float4 tab[kTailTabN * (kRepl > 0 ? kRepl : 1)];
@@ -246,7 +201,6 @@ __global__ __launch_bounds__(kThreads, MG_FWD_MINWAVES) void smf_fwd_kernel(
   // are masked with x = -inf), so the ballot counts stay in SGPRs and are complete
   const int lane = threadIdx.x & (kWave - 1);
   const int wbase = __builtin_amdgcn_readfirstlane(threadIdx.x - lane);
-#if MG_FWD_PIPE
   // Software pipeline over the grid-stride iterations: the halos of iteration k+2 (x and
   // population id) and the parameter gather of iteration k+1 are in flight while
   // iteration k is computed, so neither the id load nor the dependent gather is waited for
@@ -289,7 +243,6 @@ __global__ __launch_bounds__(kThreads, MG_FWD_MINWAVES) void smf_fwd_kernel(
       }
     }
   } else
-#endif
   for (int64_t w0 = begin + (int64_t)bid * kThreads + wbase; w0 < end;
        w0 += kFwdUnroll * stride) {
     // issue every load of this iteration before any math (one dependent round trip)
@@ -309,11 +262,7 @@ __global__ __launch_bounds__(kThreads, MG_FWD_MINWAVES) void smf_fwd_kernel(
     for (int u = 0; u < kFwdUnroll; ++u)
       halo_mass<NB, LOGSIG, REL, kRepl>(xs[u], ths[u], bins, acc, cnt, tb);
   }
-#if MG_FWD_BALLOT
   const bool counter = lane == 0;  // the counts are per wave: fold them in once
-#else
-  const bool counter = true;
-#endif
 #pragma unroll
   for (int k = 0; k < NB; ++k)
     acc[k] = (acc[k + 1] - acc[k]) + (counter ? (float)(cnt[k + 1] - cnt[k]) : 0.0f);
@@ -409,19 +358,10 @@ struct EpiArgs {
   int* advance;
 };
 
-// The epilogue as the work of ONE whole workgroup of NT threads (its own kernel, or the last
-// part of the lanes fix-up launch, LMODE 2).
-// COH: the slab rows were written by other workgroups of the SAME launch (the epilogue
-// folded into the lanes forward, MG_FOLD_EPI) with device-coherent stores: read them with
-// device-coherent loads too (past this XCD's L2, which may hold none or stale lines).
-// 1: the stand-alone epilogue reduces the slab as a flat array with coalesced loads (see
-// epilogue_block); 0: row by row.  Same-box A/B (round 4, profiles/knobs_r4/): within the
-// run-to-run spread on the owner proxy and the headline, so the row form stays
-#ifndef MG_EPI_FLAT
-#define MG_EPI_FLAT 0
-#endif
-
-template <int NB, int NT, bool COH = false, int U = 4>
+// The epilogue as the work of ONE whole workgroup of NT threads, reducing the slab row by
+// row.  (A flat-array reduction with coalesced loads measured within the run-to-run spread
+// on the owner proxy and the headline -- round 4, profiles/knobs_r4/ -- and was removed.)
+template <int NB, int NT, int U = 4>
 __device__ __forceinline__ void epilogue_block(const EpiArgs& E, const SmfBins& bins) {
   __shared__ double scratch[NB * (NT / kWave)];
   __shared__ float Sv[kXMaxFloats];
@@ -429,47 +369,14 @@ __device__ __forceinline__ void epilogue_block(const EpiArgs& E, const SmfBins& 
   __shared__ float d2[kMaxBins];
   const float* __restrict__ slab = E.slab;
   const int nrows = E.nrows, nb = E.nb;
-  if constexpr (MG_EPI_FLAT && !COH) {
-    // the slab as one flat float array: NT / NB row groups of NB threads, thread t always
-    // on bin t % NB, so every load instruction of a wave reads contiguous floats (the row
-    // form reads 64 rows 40 bytes apart); per-thread sums in element order, then the row
-    // groups of each bin in a fixed order (deterministic)
-    constexpr int G = NT / NB;
-    constexpr int TA = G * NB;
-    constexpr int UF = 16;
-    __shared__ double part[NT];
-    const int t = threadIdx.x;
-    double acc = 0.0;
-    if (t < TA) {
-      const int64_t L = (int64_t)nrows * NB;
-      int64_t i = t;
-      for (; i + (int64_t)(UF - 1) * TA < L; i += (int64_t)UF * TA) {
-        float a[UF];
-#pragma unroll
-        for (int u = 0; u < UF; ++u) a[u] = slab[i + (int64_t)u * TA];
-#pragma unroll
-        for (int u = 0; u < UF; ++u) acc += (double)a[u];
-      }
-      for (; i < L; i += TA) acc += (double)slab[i];
-    }
-    part[t] = acc;
-    __syncthreads();
-    if (t < NB) {
-      double sum = 0.0;
-      for (int m = 0; m < G; ++m) sum += part[m * NB + t];
-      Sv[t] = (float)(sum * (double)bins.scale[t]);
-    }
-  } else {
+  {
     double v[NB];
 #pragma unroll
     for (int k = 0; k < NB; ++k) v[k] = 0.0;
     // rows U at a time with every load issued before the first add (one memory round trip
     // per U rows instead of one per row); the per-thread order of the sums is the row order
     // whatever U is (the same bits)
-    auto ld = [&](int64_t i) -> float {
-      if constexpr (COH) return __hip_atomic_load(slab + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      else return slab[i];
-    };
+    auto ld = [&](int64_t i) -> float { return slab[i]; };
     int r = threadIdx.x;
     for (; r + (U - 1) * NT < nrows; r += U * NT) {
       float a[U][NB];
@@ -523,23 +430,19 @@ __device__ __forceinline__ void epilogue_block(const EpiArgs& E, const SmfBins& 
 
 template <int NB>
 __global__ __launch_bounds__(kEpiThreads) void smf_epilogue_kernel(EpiArgs E, SmfBins bins) {
-  epilogue_block<NB, kEpiThreads, false, MG_EPI_UNROLL>(E, bins);
+  epilogue_block<NB, kEpiThreads, MG_EPI_UNROLL>(E, bins);
 }
 
 // Per-halo VJP contributions in the scaled coordinate w = z*kWScale:
 //   A += sum_e h_e exp2(-w_e^2),   B += sum_e h_e exp2(-w_e^2) w_e
 // (h_e already carries 1/sqrt(2 pi); B is converted back to z units in pop_grad).
-// MG_VJP_EP: edges two at a time in packed fp32 (v_pk_fma / v_pk_mul / v_pk_add on the
+// Edges two at a time in packed fp32 (v_pk_fma / v_pk_mul / v_pk_add on the
 // pair (edge 2i, edge 2i+1), as in the lanes forward's EdgePairs), so w, w^2, h*g and both
 // accumulations cost one issue per pair; v_exp stays per element.
-#ifndef MG_VJP_EP
-#define MG_VJP_EP 1
-#endif
 template <int NB, bool LOGSIG>
 __device__ __forceinline__ void halo_vjp(float x, float2 th, float inv, const float (&h)[NB + 1],
                                          const SmfBins& b, float& A, float& B) {
   const float nmi = -(x + th.x) * inv;
-#if MG_VJP_EP
   constexpr int NP = (NB + 1) / 2;
   v2f Ap = (v2f)(0.0f), Bp = (v2f)(0.0f);
 #pragma unroll
@@ -566,15 +469,6 @@ __device__ __forceinline__ void halo_vjp(float x, float2 th, float inv, const fl
   }
   A += Ap.x + Ap.y;
   B += Bp.x + Bp.y;
-#else
-#pragma unroll
-  for (int e = 0; e <= NB; ++e) {
-    const float w = fmaf(b.edge[e], inv, nmi);
-    const float t = h[e] * fast_exp2(-w * w);
-    A += t;
-    B = fmaf(t, w, B);
-  }
-#endif
 }
 
 // inv is the scaled inverse sigma (kWScale / sigma); A, B from halo_vjp.
@@ -864,11 +758,7 @@ __device__ __forceinline__ void lane_halo2(v2f x, float ninv, float mua, const S
     v2f sg;
     sg.x = __builtin_copysignf(g.x, n.x);
     sg.y = __builtin_copysignf(g.y, n.y);
-#if MG_LANES_ACC2
-    acc2[e] = p * sg + acc2[e];
-#else
     acc2[e].x = fmaf(p.y, sg.y, fmaf(p.x, sg.x, acc2[e].x));
-#endif
     cnt[e] += __builtin_popcountll(__builtin_amdgcn_ballot_w64(n.x < 0.0f)) +
               __builtin_popcountll(__builtin_amdgcn_ballot_w64(n.y < 0.0f));
     if constexpr (RESID) {
@@ -978,7 +868,7 @@ __device__ __forceinline__ void lane_halo_ep(float x0, float x1, float ninv, flo
 }
 
 // ---------------------------------------------------------- Euler-Maclaurin bin masses
-// MG_FWD_EM (absolute contract, uniformly spaced edges): inside a lanes group every halo of
+// Euler-Maclaurin path (absolute contract, uniformly spaced edges): inside a lanes group every halo of
 // a lane shares the lane's sigma, so the bin width in sigma units h = delta / sigma is a
 // lane constant.  The mass of bin k is then the integral of the Gaussian over one panel of
 // width h, evaluated by the Euler-Maclaurin formula from the Gaussian factor and its odd
@@ -1002,9 +892,6 @@ __device__ __forceinline__ void lane_halo_ep(float x0, float x1, float ninv, flo
 // relative-tail contract) runs the per-edge tail evaluation instead (the ballot is
 // wave-uniform).  The VJP residuals agree with the per-edge exponentials to the chain's
 // rounding (~1e-6 relative), inside the VJP's contract.
-#ifndef MG_FWD_EM
-#define MG_FWD_EM 1
-#endif
 constexpr float kEmHMax = 0.5f;
 constexpr float kInvSqrt2Pi = 0.39894228040143268f;
 
@@ -1096,20 +983,15 @@ __device__ __forceinline__ void em_halo(float nm, float inv, float dw4, float a1
   }
 }
 
-// MG_EM_SCHED_BARRIER: keep the scheduler from interleaving consecutive halos (their
+// Keep the scheduler from interleaving consecutive halos (their
 // temporaries would double the register footprint of the pipelined-update kernel)
-#ifndef MG_EM_SCHED_BARRIER
-#define MG_EM_SCHED_BARRIER 1
-#endif
 template <int NB, bool RESID>
 __device__ __forceinline__ void lane_halo_em(float x, const EmLane& L, float nma,
                                              const SmfBins& b, v2f (&F)[EdgePairs<NB>::NV],
                                              v2f (&Wa)[EdgePairs<NB>::NV],
                                              v2f (&E)[EdgePairs<NB>::NV]) {
   em_halo<NB, RESID>(fmaf(x, -L.inv, nma), L.inv, L.dw4, L.a1, L.a3, L.a5, b, F, Wa, E);
-#if MG_EM_SCHED_BARRIER
   __builtin_amdgcn_sched_barrier(0);
-#endif
 }
 
 // Per-edge evaluation of ONE halo (absolute contract, scalar) into the edge-pair
@@ -1145,9 +1027,7 @@ __device__ __forceinline__ void lane_halo_exact1(float x, float ninv, float mua,
       }
     }
   }
-#if MG_EM_SCHED_BARRIER
   __builtin_amdgcn_sched_barrier(0);
-#endif
 }
 
 // End of a group: apply the lane constants Q_j to the pair sums (F, Wa become the true
@@ -1198,7 +1078,7 @@ __device__ __forceinline__ void em_group_end(const EmLane& L, v2f (&F)[EdgePairs
 }
 
 // ================================================= tiles VJP, recurrence + owner segments
-// MG_VJP_REC (default on, uniform unpadded bins): the tiles VJP of the hashed shards with
+// Uniform unpadded bins: the tiles VJP of the hashed shards with
 // (1) the Gaussian factors of one halo's equally spaced edges from one seed pair at the
 //     middle edges and the exact ratio recurrence f_{e+2} = f_e exp2(-4 dw w_{e+1}) (the
 //     ratio itself advances by the constant exp2(-8 dw^2)): 6 transcendentals per halo
@@ -1215,9 +1095,6 @@ __device__ __forceinline__ void em_group_end(const EmLane& L, v2f (&F)[EdgePairs
 // The seed sits at the middle pair, so a seed that underflows (|z| > 13) is at least
 // 13 - NB/2 h sigma away from every edge; with h = delta/sigma <= 1 (dw <= kWScale, checked
 // wave-uniformly, else the per-edge path of halo_vjp) the dropped terms are below 3e-15.
-#ifndef MG_VJP_REC
-#define MG_VJP_REC 1
-#endif
 
 template <int NB>
 struct VjpPairs {
@@ -1474,56 +1351,30 @@ __global__ __launch_bounds__(kThreads, MG_VJP_REC_MINWAVES) void smf_vjp_tiles_r
 // Measured on MI355X (1e7 params, 1.34e8 halos, internal order, with residuals): the
 // edge-pair path at 4 waves/SIMD (118 VGPRs, no spills) 595 us vs 615-624 us for the
 // compiler-packed scalar path at 6 waves; at 5 or 6 waves the edge-pair path spills.
-#ifndef MG_FWD_PRIO
-#define MG_FWD_PRIO 1  // static-list issue-priority feedback (tools/ab_prio.sh)
-#endif
-#ifndef MG_LANES_EP
-#define MG_LANES_EP 1
-#endif
-// How the Euler-Maclaurin residual forwards evaluate a group outside the EM range:
-//   0: inline per-edge fallback (LMODE 0; costs the hot loop registers and spills),
-//   1: deferral list + fix-up launch (LMODE 1 + 2, round 3; the fix-up launch is narrow),
-//   2: out-of-line per-edge call inside the main launch (LMODE 3, default): full machine
-//      parallelism at any deferral fraction, no fix-up launch, no list atomics.
-#ifndef MG_LANES_DEFER
-#define MG_LANES_DEFER 2
-#endif
-// 1: the sumstat epilogue folded into the last workgroup of the lanes forward launch when
-// there is no fix-up launch (smf_forward_lanes); 0 (default): its own one-workgroup launch.
-// Measured alternating on one box (docs/design.md "Open performance items"): headline
-// 0.4352-0.4357 vs 0.4352-0.4364 ms/step, owner proxy 0.0626-0.0628 vs 0.0618-0.0619 --
-// the folded form is not faster, so it is compiled out by default.
-#ifndef MG_FOLD_EPI
-#define MG_FOLD_EPI 0
-#endif
-// LMODE of the main launch of the EM residual forwards (0 in builds without them)
-constexpr int kLanesMainMode =
-    !(MG_FWD_EM && MG_LANES_EP) ? 0 : MG_LANES_DEFER == 1 ? 1 : MG_LANES_DEFER == 2 ? 3 : 0;
+// The Euler-Maclaurin residual forwards evaluate a group outside the EM range by an
+// out-of-line per-edge call inside the main launch (LMODE 3): full machine parallelism at
+// any out-of-range fraction, no fix-up launch, no list atomics.  Measured and removed in
+// round 5 (docs/design.md "Open performance items"): the inline per-edge fallback (LMODE 0
+// with residuals: it costs the hot loop registers and spills), the round-3 deferral list +
+// narrow fix-up launch (LMODE 1 + 2), and the sumstat epilogue folded into the last
+// workgroup of the lanes forward (headline 0.4352-0.4357 vs 0.4352-0.4364 ms/step, owner
+// proxy 0.0626-0.0628 vs 0.0618-0.0619: not faster than its own one-workgroup launch).
+constexpr int kLanesMainMode = 3;
 
-// Packed two-halo path: 10% fewer VALU cycles per halo pair, but it needs 108 VGPRs
-// (4 waves/SIMD) to avoid spills; measured on MI355X it ties the scalar path (690 vs
-// 692 us at 1.34e8 halos), so the scalar path at 6 waves/SIMD stays the default.
-#ifndef MG_LANES_V2
-#define MG_LANES_V2 0
-#endif
-#ifndef MG_LANES_ACC2
-#define MG_LANES_ACC2 0  // 1: one bin partial per halo of the pair (more registers)
-#endif
+// Minimum resident waves per SIMD of the lanes forward: the edge-pair path needs up to 128
+// VGPRs (4 waves/SIMD) to avoid spills; at 5 or 6 waves it spills.
 #ifndef MG_LANES_MINWAVES
-#define MG_LANES_MINWAVES (MG_LANES_EP ? 4 : 6)
+#define MG_LANES_MINWAVES 4
 #endif
 #ifndef MG_LANES_UNROLL
 #define MG_LANES_UNROLL 2
 #endif
 constexpr int kLanesUnroll = MG_LANES_UNROLL;
 
-// MG_LANES_BUF: the lanes kernel addresses xi, slot_pop and the residuals through buffer
+// The lanes kernel addresses xi, slot_pop and the residuals through buffer
 // descriptors (4 SGPRs, rebuilt per group) and one 32-bit lane offset, instead of the 64-bit
 // per-lane pointers the compiler otherwise hoists into VGPR pairs (two VGPRs each): that is
 // what the pipelined-update instantiation needs to stay within 128 VGPRs without spills.
-#ifndef MG_LANES_BUF
-#define MG_LANES_BUF 1
-#endif
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* p) {
   // raw buffer, stride 0; range 2 GB from the base (every access is base + lane*4 + small)
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, 0x7fffffff, 0x00020000);
@@ -1538,54 +1389,23 @@ __device__ __forceinline__ void buf_store_f32(__amdgpu_buffer_rsrc_t r, int voff
   __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, voff, soff, 0);
 }
 
-// Halo j of a lane (sentinel past the end).  MG_LANES_UNCOND: the load itself is
-// unconditional (the host pads xi by 16 rows) and the value is selected, so there is no
-// branch around it and the compiler can count the outstanding loads exactly
-// (s_waitcnt vmcnt(N) instead of vmcnt(0) at every loop back-edge).
-#ifndef MG_LANES_UNCOND
-#define MG_LANES_UNCOND 0
-#endif
-// (the select happens at the use, lane_use, so the wait lands there and not at the load)
-#if MG_LANES_BUF
+// Halo j of a lane (sentinel past the end).  The load is a buffer load at a wave-uniform
+// row offset; an unconditional load with the select at the use measured no faster and was
+// removed in round 5.
 struct LaneSrc {  // this group's halos: descriptor at the group base, lane byte offset
   __amdgpu_buffer_rsrc_t r;
   int voff;
 };
 __device__ __forceinline__ float lane_load(const LaneSrc& xp, int j, int len) {
-#if MG_LANES_UNCOND
-  return buf_load_f32(xp.r, xp.voff, j * kWave * 4);
-#else
   return j < len ? buf_load_f32(xp.r, xp.voff, j * kWave * 4) : kLaneSentinel;
-#endif
 }
-#else
-using LaneSrc = const float*;
-__device__ __forceinline__ float lane_load(const float* xp, int j, int len) {
-#if MG_LANES_UNCOND
-  return xp[(int64_t)j * kWave];
-#else
-  return j < len ? xp[(int64_t)j * kWave] : kLaneSentinel;
-#endif
-}
-#endif
 __device__ __forceinline__ float lane_use(float v, int j, int len) {
-#if MG_LANES_UNCOND
-  return j < len ? v : kLaneSentinel;
-#else
   return v;
-#endif
 }
 
-// Residual stores: MG_LANES_NTSTORE writes them non-temporal (streamed past the caches).
-#ifndef MG_LANES_NTSTORE
-#define MG_LANES_NTSTORE 0
-#endif
+// Residual stores (plain stores: non-temporal ones measured no faster, removed in round 5).
 __device__ __forceinline__ void resid_store(float* p, float v) {
-#if MG_LANES_NTSTORE
-  __builtin_nontemporal_store(v, p);
-#else
   *p = v;
-#endif
 }
 
 // Diagnostics build (-DMG_FWD_TRACE): every wavefront of the lanes forward records its
@@ -1694,14 +1514,12 @@ __device__ __attribute__((noinline)) LaneGroupSums<NB> lanes_group_exact(
   return o;
 }
 
-// LMODE (Euler-Maclaurin residual forwards, MG_LANES_DEFER): 0 = plain; 3 = CALL: a group
-// outside the EM range is evaluated by lanes_group_exact (out of line); 1 = DEFER: a group
-// outside the EM range is not evaluated here but appended to the device list `defer`
-// ([count, done ticket, group ids...]) -- the kernel then carries no per-edge fallback code
-// (which cost ~3.5% of the headline step in registers although the headline data never
-// takes it: profiles/em_forward/, 2276-2291 vs 2204-2210 steps/s); 2 = LIST: the fix-up
-// launch that follows, over the listed groups only (EM + per-edge fallback, residuals and
-// its own slab rows), whose last workgroup resets the list for the next launch.
+// LMODE: 0 = plain (forwards without residuals: Euler-Maclaurin where the group is in
+// range, inline per-edge tails otherwise); 3 = CALL (EM residual forwards): a group outside
+// the EM range is evaluated by lanes_group_exact, out of line -- an inline fallback cost
+// ~3.5% of the headline step in registers although the headline data never takes it
+// (profiles/em_forward/); 4 = PER-EDGE: no EM path, every group by the packed two-halo
+// per-edge tails, for shards where most lane groups are outside the EM range anyway.
 template <int NB, bool LOGSIG, bool REL, bool RESID, bool UPD = false, int LMODE = 0,
           bool BND = false>
 __global__ __launch_bounds__(kThreads, MG_LANES_MINWAVES) void smf_fwd_lanes_kernel(
@@ -1710,27 +1528,17 @@ __global__ __launch_bounds__(kThreads, MG_LANES_MINWAVES) void smf_fwd_lanes_ker
     const int32_t* __restrict__ fwd_order, const float2* __restrict__ theta, int64_t g0,
     int64_t g1, SmfBins bins, float* __restrict__ slab, float* __restrict__ resid,
     const int32_t* __restrict__ wave_start, int* __restrict__ queues, int nq,
-    LanesUpdate upd = LanesUpdate{}, int* __restrict__ defer = nullptr, EpiArgs epi = EpiArgs{}) {
+    LanesUpdate upd = LanesUpdate{}) {
   static_assert(!UPD || RESID, "the pipelined update reads the residuals it overwrites");
   static_assert(!BND || UPD, "bounds belong to the pipelined update");
-  static_assert(LMODE == 0 || LMODE == 4 || (RESID && MG_FWD_EM && MG_LANES_EP && !REL),
-                "deferral: EM residual forwards");
-  static_assert(LMODE != 2 || !UPD, "the fix-up launch evaluates updated groups");
-  if constexpr (LMODE == 2) {  // the listed groups, grid-strided
-    fwd_order = defer + 2;
-    g0 = 0;
-    g1 = __builtin_amdgcn_readfirstlane(__hip_atomic_load(defer, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-  }
-  // signed-tail table (absolute contract): 16 replicas (conflict-free reads), 8 next to
-  // the pipelined update's staging buffer (LDS budget of 4 workgroups per CU)
-  // LMODE 4 (PER-EDGE): no Euler-Maclaurin path; every group by the packed two-halo
-  // per-edge tails (the kernel of builds with MG_FWD_EM=0), for shards where most lane
-  // groups are outside the EM range anyway
-  constexpr bool kEmOn = MG_FWD_EM && LMODE != 4;
-  constexpr int kRepl =
-      (!REL && MG_LANES_EP && !kEmOn && (MG_FWD_TAB >= 2 || (MG_FWD_TAB == 1 && !RESID)))
-          ? (UPD ? 8 : 16) : 0;  // (with the EM path the fallback is the lean per-edge path)
-  constexpr bool kEm = kEmOn && MG_LANES_EP && !REL;
+  static_assert(LMODE == 0 || LMODE == 3 || LMODE == 4, "lanes mode");
+  static_assert(LMODE != 3 || (RESID && !REL), "CALL: EM residual forwards");
+  // signed-tail table (absolute contract, per-edge forwards without residuals): 16
+  // replicas (conflict-free reads), 8 next to the pipelined update's staging buffer (LDS
+  // budget of 4 workgroups per CU); with the EM path the fallback is the lean per-edge path
+  constexpr bool kEmOn = LMODE != 4;
+  constexpr int kRepl = (!REL && !kEmOn && !RESID) ? (UPD ? 8 : 16) : 0;
+  constexpr bool kEm = kEmOn && !REL;
   const float4* tb = nullptr;
   if constexpr (kRepl > 0) {
     __shared__ float4 tab[kTailTabN * (kRepl > 0 ? kRepl : 1)];
@@ -1745,17 +1553,11 @@ __global__ __launch_bounds__(kThreads, MG_LANES_MINWAVES) void smf_fwd_lanes_ker
     acc[k] = 0.0f;
     cnt[k] = 0;
   }
-#if MG_LANES_EP
   using EP = EdgePairs<NB>;
   static_assert(kLanesUnroll % 2 == 0, "edge-pair path takes halos two at a time");
   v2f accp[EP::NV];
 #pragma unroll
   for (int k = 0; k < EP::NV; ++k) accp[k] = (v2f)(0.0f);
-#elif MG_LANES_V2
-  v2f acc2[NB + 1];
-#pragma unroll
-  for (int k = 0; k <= NB; ++k) acc2[k] = (v2f)(0.0f);
-#endif
   const int lane = threadIdx.x & (kWave - 1);
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t nwaves = (int64_t)gridDim.x * (kThreads / kWave);
@@ -1800,16 +1602,11 @@ __global__ __launch_bounds__(kThreads, MG_LANES_MINWAVES) void smf_fwd_lanes_ker
   int64_t k_next = g1;
   int64_t g = 0;
   float2 th = make_float2(0.f, 0.f);
-#if MG_LANES_BUF
   const int lane4 = lane * 4;
   LaneSrc xp{buf_rsrc(xi), lane4};
   auto slot_of = [&](int64_t kk) {
     return buf_load_i32(buf_rsrc(slot_pop + (int64_t)fwd_order[kk] * kWave), lane4, 0);
   };
-#else
-  LaneSrc xp = xi;
-  auto slot_of = [&](int64_t kk) { return slot_pop[(int64_t)fwd_order[kk] * kWave + lane]; };
-#endif
   int len = 0;
   int c_next = 0;
   int c_cur = -1;
@@ -1924,11 +1721,7 @@ __global__ __launch_bounds__(kThreads, MG_LANES_MINWAVES) void smf_fwd_lanes_ker
     c_cur = c;
     stage_update(g, c);
     th = theta[c < 0 ? 0 : c];
-#if MG_LANES_BUF
     xp.r = buf_rsrc(xi + group_base[g]);
-#else
-    xp = xi + group_base[g] + lane;
-#endif
     len = group_len[g];
 #pragma unroll
     for (int u = 0; u < kLanesUnroll; ++u) xn[u] = lane_load(xp, u, len);
@@ -1943,50 +1736,31 @@ __global__ __launch_bounds__(kThreads, MG_LANES_MINWAVES) void smf_fwd_lanes_ker
       fetch_next_slot();
     }
   }
-#if MG_FWD_PRIO
   const int64_t k_first = k;
-#endif
   while (k < g1) {
-#if MG_FWD_PRIO
     // Static lists: the wave's issue priority falls as its list drains, so the SIMD's
     // arbiter prefers the waves that are behind instead of always the oldest one (which
     // leaves the youngest wave running the tail alone, profiles/fwd_wave_timeline.md).
     if (!dyn && wave_start) {
-#if MG_FWD_PRIO == 2
-      // longest-remaining-first: priority = groups left after this one (clamped to 3)
-      const int lvl = (int)min((int64_t)3, g1 - k - 1);
-#else
       const int64_t tot = g1 - k_first;
       const int lvl = (int)((4 * (g1 - k) - 1) / tot);
-#endif
       if (lvl >= 3) __builtin_amdgcn_s_setprio(3);
       else if (lvl == 2) __builtin_amdgcn_s_setprio(2);
       else if (lvl == 1) __builtin_amdgcn_s_setprio(1);
       else __builtin_amdgcn_s_setprio(0);
     }
-#endif
     const int64_t gc = g;
     const float ninv = -inv_sigma<LOGSIG>(th.y) * kWScale;
     const float mua = -th.x * ninv;
-#if MG_LANES_EP
     v2f Gp[EP::NV], Wp[EP::NV];
 #pragma unroll
     for (int e = 0; e < EP::NV; ++e) {
       Gp[e] = (v2f)(0.0f);
       Wp[e] = (v2f)(0.0f);
     }
-#else
-    float G[NB + 1], W[NB + 1];
-#pragma unroll
-    for (int e = 0; e <= NB; ++e) {
-      G[e] = 0.0f;
-      W[e] = 0.0f;
-    }
-#endif
     // Euler-Maclaurin path (see em_halo) when every occupied lane's bin width is inside
     // kEmHMax; the ballot makes the choice wave-uniform
     bool em = false;
-#if MG_LANES_EP
     if constexpr (kEm) {
       const float inv = -ninv;
       const bool bad = c_cur >= 0 && !(bins.delta * inv * (1.0f / kWScale) <= kEmHMax);
@@ -2010,15 +1784,9 @@ __global__ __launch_bounds__(kThreads, MG_LANES_MINWAVES) void smf_fwd_lanes_ker
       }
       em_group_end<NB>(eml, Gp, Wp, Ep, accp);
     }
-#endif
     // the next kLanesUnroll loads are in flight while the current halos are computed;
     // past-the-end halos are the sentinel (exact zero contribution)
-    if constexpr (LMODE == 1) {
-      if (!em && lane == 0) {  // outside the EM range: the fix-up launch evaluates it
-        const int slot = atomicAdd(defer, 1);
-        defer[2 + slot] = (int)gc;
-      }
-    } else if constexpr (LMODE == 3) {
+    if constexpr (LMODE == 3) {
       if (!em) {  // outside the EM range: per-edge tails, out of line (stores the residuals)
         const LaneGroupSums<NB> o = lanes_group_exact<NB>(
             xi + group_base[gc], len, lane_use(xn[0], 0, len), lane_use(xn[1], 1, len), ninv,
@@ -2030,11 +1798,7 @@ __global__ __launch_bounds__(kThreads, MG_LANES_MINWAVES) void smf_fwd_lanes_ker
         for (int e = 0; e <= NB; ++e) cnt[e] += __builtin_amdgcn_readfirstlane(o.cnt[e]);
       }
     } else
-#ifdef MG_FWD_EM_ONLY
-    if (!kEm)
-#else
     if (!em)
-#endif
     for (int j = 0; j < len; j += kLanesUnroll) {
       float xc[kLanesUnroll];
 #pragma unroll
@@ -2043,7 +1807,6 @@ __global__ __launch_bounds__(kThreads, MG_LANES_MINWAVES) void smf_fwd_lanes_ker
         const int jn = j + kLanesUnroll + u;
         xn[u] = lane_load(xp, jn, len);
       }
-#if MG_LANES_EP
       if constexpr (kEm) {  // lean fallback of the Euler-Maclaurin kernels
 #pragma unroll
         for (int u = 0; u < kLanesUnroll; ++u)
@@ -2054,20 +1817,6 @@ __global__ __launch_bounds__(kThreads, MG_LANES_MINWAVES) void smf_fwd_lanes_ker
           lane_halo_ep<NB, LOGSIG, REL, RESID, kRepl>(xc[u], xc[u + 1], ninv, mua, bins, accp,
                                                       cnt, Gp, Wp, tb);
       }
-#elif MG_LANES_V2
-      static_assert(kLanesUnroll % 2 == 0, "packed path takes halo pairs");
-#pragma unroll
-      for (int u = 0; u < kLanesUnroll; u += 2) {
-        v2f xv;
-        xv.x = xc[u];
-        xv.y = xc[u + 1];
-        lane_halo2<NB, LOGSIG, REL, RESID>(xv, ninv, mua, bins, acc2, cnt, G, W);
-      }
-#else
-#pragma unroll
-      for (int u = 0; u < kLanesUnroll; ++u)
-        lane_halo<NB, LOGSIG, REL, RESID>(xc[u], ninv, mua, bins, acc, cnt, G, W);
-#endif
     }
     const int64_t kn = k_next;
 #ifdef MG_FWD_TRACE
@@ -2075,15 +1824,10 @@ __global__ __launch_bounds__(kThreads, MG_LANES_MINWAVES) void smf_fwd_lanes_ker
 #endif
     if constexpr (!UPD)
       if (kn < g1) load_group(kn, c_next);
-    // group-major [g][2 (NB+1)][64]: one block per group (LMODE 1: deferred groups are
-    // stored by the fix-up launch; LMODE 3: by lanes_group_exact)
-    if (RESID && ((LMODE != 1 && LMODE != 3) || em)) {
-#if MG_LANES_BUF
+    // group-major [g][2 (NB+1)][64]: one block per group (LMODE 3: the groups outside the
+    // EM range are stored by lanes_group_exact)
+    if (RESID && (LMODE != 3 || em)) {
       const __amdgpu_buffer_rsrc_t rr = buf_rsrc(resid + gc * (2 * (NB + 1) * kWave));
-#else
-      float* rg = resid + gc * (2 * (NB + 1) * kWave) + lane;
-#endif
-#if MG_LANES_EP
       float G[NB + 1], W[NB + 1];
 #pragma unroll
       for (int i = 0; i < EP::NP; ++i) {
@@ -2096,16 +1840,10 @@ __global__ __launch_bounds__(kThreads, MG_LANES_MINWAVES) void smf_fwd_lanes_ker
         G[NB] = Gp[EP::NP].x + Gp[EP::NP].y;
         W[NB] = Wp[EP::NP].x + Wp[EP::NP].y;
       }
-#endif
 #pragma unroll
       for (int e = 0; e <= NB; ++e) {
-#if MG_LANES_BUF
         buf_store_f32(rr, lane4, e * kWave * 4, G[e]);
         buf_store_f32(rr, lane4, (NB + 1 + e) * kWave * 4, W[e]);
-#else
-        resid_store(rg + e * kWave, G[e]);
-        resid_store(rg + (NB + 1 + e) * kWave, W[e]);
-#endif
       }
     }
     k = kn;
@@ -2121,17 +1859,12 @@ __global__ __launch_bounds__(kThreads, MG_LANES_MINWAVES) void smf_fwd_lanes_ker
       }
     }
   }
-#if MG_LANES_EP
 #pragma unroll
   for (int i = 0; i < EP::NP; ++i) {
     acc[2 * i] = accp[i].x;
     acc[2 * i + 1] = accp[i].y;
   }
   if constexpr (EP::NX) acc[NB] = accp[EP::NP].x + accp[EP::NP].y;
-#elif MG_LANES_V2
-#pragma unroll
-  for (int k = 0; k <= NB; ++k) acc[k] = acc2[k].x + acc2[k].y;
-#endif
 #ifdef MG_FWD_TRACE
   if (lane == 0 && w_id < kTraceWaves) {
     g_fwd_trace[3 * w_id] = t_start;
@@ -2146,63 +1879,14 @@ __global__ __launch_bounds__(kThreads, MG_LANES_MINWAVES) void smf_fwd_lanes_ker
   __shared__ float scratch[NB * (kThreads / kWave)];
   float(&bin)[NB] = *reinterpret_cast<float(*)[NB]>(acc);
   block_sum_n<NB>(bin, scratch);
-  // folded epilogue (MG_FOLD_EPI; not with the deferral list, whose fix-up launch carries
-  // it): the host passes epi.on and a self-resetting ticket in `defer`
-  constexpr bool kFoldable = MG_FOLD_EPI && LMODE != 1 && LMODE != 2;
-  const bool fold = kFoldable && epi.on;
   if (threadIdx.x == 0) {
-    if (fold) {
-      // device-coherent row stores (written through this XCD's L2), acknowledged before the
-      // ticket: no release fence, which would write back every dirty L2 line of the launch
-      // (the fused update's theta / m / v / residual stores; profiles/epilogue_in_forward/)
 #pragma unroll
-      for (int k = 0; k < NB; ++k)
-        __hip_atomic_store(slab + (int64_t)blockIdx.x * NB + k, acc[k], __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-#pragma unroll
-      for (int k = 0; k < NB; ++k) slab[(int64_t)blockIdx.x * NB + k] = acc[k];
-    }
-    if constexpr (LMODE == 2) {
-      // every workgroup read the count at its start; the last one to finish resets the
-      // list for the next step's launch (self-resetting: graph-replay safe)
-      if (gridDim.x == 1 || atomicAdd(defer + 1, 1) == (int)gridDim.x - 1) {
-        __hip_atomic_store(defer, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(defer + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
-  }
-  if constexpr (LMODE == 2) {
-    // single-workgroup fix-up launch with the sumstat epilogue folded in (one launch per
-    // step fewer): this workgroup's own slab row is the last one the epilogue reads
-    if (epi.on && gridDim.x == 1) {  // (the host launches the folded form with one workgroup)
-      __syncthreads();
-      epilogue_block<NB, kThreads>(epi, bins);
-    }
-  }
-  if constexpr (kFoldable) {
-    if (fold) {
-      // the last workgroup to finish reduces every row (its own included) and runs the
-      // epilogue: one launch per step instead of two
-      __shared__ int last_wg;
-      if (threadIdx.x == 0) {
-        uc_release();  // this workgroup's row stores acknowledged
-        last_wg = atomicAdd(defer, 1) == (int)gridDim.x - 1;
-      }
-      __syncthreads();
-      if (last_wg) {
-        if (threadIdx.x == 0) __hip_atomic_store(defer, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        epilogue_block<NB, kThreads, true>(epi, bins);
-      }
-    }
+    for (int k = 0; k < NB; ++k) slab[(int64_t)blockIdx.x * NB + k] = acc[k];
   }
 }
 
 // Residual VJP over slots [s0, s1): whole populations write their gradient, parts of
 // split populations write partials[part] (summed by smf_vjp_finalize_kernel).
-#ifndef MG_VJP_LANES_PERSIST
-#define MG_VJP_LANES_PERSIST 1
-#endif
 // Fused VJP + Adam (unbounded) for shards whose populations are all whole: a lane that
 // has its population's gradient applies the Adam update to the population's (a, s) pair
 // directly -- theta, m, v and the trajectory row -- so the gradient never round-trips
@@ -2252,7 +1936,6 @@ __global__ __launch_bounds__(kThreads) void smf_vjp_lanes_kernel(
   }
   constexpr int R = 2 * (NB + 1);
   const int lane = threadIdx.x & (kWave - 1);
-#if MG_VJP_LANES_PERSIST
   // Persistent wavefronts, one group per iteration, the next group's residuals in flight
   // while the current one is contracted and written.  XCD-aware: workgroups are
   // dispatched round-robin over the kXcds L2 domains, so XCD x = blockIdx % kXcds takes
@@ -2307,22 +1990,6 @@ __global__ __launch_bounds__(kThreads) void smf_vjp_lanes_kernel(
     }
     g = gn;
   }
-#else
-  const int64_t s = s0 + (int64_t)blockIdx.x * kThreads + threadIdx.x;
-  if (s >= s1) return;
-  const int c = slot_pop[s];
-  const float* rg = resid + (s >> 6) * (R * kWave) + (s & (kWave - 1));
-  float A = 0.0f, B = 0.0f;
-#pragma unroll
-  for (int e = 0; e <= NB; ++e) {
-    A = fmaf(hvec[e], rg[e * kWave], A);
-    B = fmaf(hvec[e], rg[(NB + 1 + e) * kWave], B);
-  }
-  if (c < 0) return;
-  const int part = slot_part[s];
-  if (part >= 0) partials[part] = make_float2(A, B);
-  else grad[c] = pop_grad<LOGSIG>(theta[c], A, B);
-#endif
 }
 
 // VJP by recomputation over the lanes layout (no residuals): one wavefront per 64-slot
@@ -2649,7 +2316,7 @@ void smf_vjp(torch::Tensor x, c10::optional<torch::Tensor> pop, torch::Tensor th
   float2* gp = reinterpret_cast<float2*>(grad.data_ptr<float>());
   float2* pa = partials.numel() ? reinterpret_cast<float2*>(partials.data_ptr<float>()) : nullptr;
   // the recurrence kernel needs uniform, unpadded bins (b.delta > 0) and population ids
-  const bool rec = MG_VJP_REC && b.delta > 0.0f && has_pop;
+  const bool rec = b.delta > 0.0f && has_pop;
   bool fused = false;
   if (!exchange.empty()) {
     const TwoShotPack xs = twoshot_unpack(exchange);
@@ -2777,10 +2444,6 @@ torch::Tensor smf_fwd_trace() {
 }
 
 // ------------------------------------------------------------------ lanes host side
-// How the EM residual forwards handle out-of-range groups (MG_LANES_DEFER): 1 = deferral
-// list + fix-up launch (the caller provides the list and fix-up slab rows), 2 = out-of-line
-// call inside the main launch, 0 = inline fallback.
-int64_t smf_lanes_fallback_mode() { return MG_LANES_DEFER; }
 
 int64_t smf_fwd_lanes_max_blocks(int64_t nb, bool log_sigma, bool rel_tail, bool resid) {
   const int nbp = padded_bins((int)nb);
@@ -2830,7 +2493,6 @@ int64_t smf_forward_lanes(torch::Tensor xi, torch::Tensor slot_pop, torch::Tenso
                        c10::optional<torch::Tensor> queues,
                        c10::optional<std::vector<torch::Tensor>> update,
                        std::vector<double> update_scalars,
-                       c10::optional<torch::Tensor> defer, int64_t fix_blocks,
                        std::vector<torch::Tensor> epi_tensors, std::vector<double> epi_scalars,
                        std::vector<int64_t> epi_peers, bool per_edge) {
   check_dev(xi, "xi", at::kFloat);
@@ -2881,37 +2543,17 @@ int64_t smf_forward_lanes(torch::Tensor xi, torch::Tensor slot_pop, torch::Tenso
   const SmfBins b = make_bins(edges, scale, nbp);
   auto stream = at::hip::getCurrentHIPStream();
   const float2* tp = reinterpret_cast<const float2*>(theta.data_ptr<float>());
-  // Residual forwards with a deferral list (MG_LANES_DEFER 1, see LMODE): the main launch
-  // defers groups outside the Euler-Maclaurin range, then a fix-up launch of fix_blocks
-  // workgroups evaluates them into slab rows [nblocks, nblocks + fix_blocks).  Without
-  // uniform bins the main launch keeps its own per-edge path and no fix-up launch runs
-  // (fixb = 0: the rows are neither written nor counted).  With MG_LANES_DEFER 2 the list
-  // is ignored (lanes_fallback_mode() tells the caller not to allocate the rows).
-  int* dp = nullptr;
-  if (MG_LANES_DEFER == 1 && defer.has_value() && defer->defined()) {
-    TORCH_CHECK(has_resid, "the deferral list is for residual forwards");
-    check_dev(*defer, "defer", at::kInt);
-    TORCH_CHECK(defer->numel() >= 2 + ng, "defer: [count, ticket, one slot per group]");
-    TORCH_CHECK(fix_blocks >= 1 && fix_blocks <= 65535, "bad fix-up block count");
-    TORCH_CHECK(slab.numel() >= (nblocks + fix_blocks) * nbp, "slab too small for the fix-up rows");
-    dp = defer->data_ptr<int>();
-  }
   // the Euler-Maclaurin residual forwards: out-of-range groups through the out-of-line call
-  // (LMODE 3, MG_LANES_DEFER 2) or the deferral list (LMODE 1 + 2, MG_LANES_DEFER 1)
-  const bool em_resid = has_resid && MG_FWD_EM && MG_LANES_EP && !rel_tail && b.delta > 0.0f;
-  // per_edge (the caller's choice when most groups are outside the EM range, e.g. a fit
-  // with narrow populations everywhere): LMODE 4, the per-edge kernel for every group
-  const bool ledge = per_edge && em_resid && MG_LANES_EP;
-  const bool lmode = !ledge && dp != nullptr && MG_LANES_DEFER == 1 && em_resid;
-  const bool lcall = !ledge && MG_LANES_DEFER == 2 && em_resid;
-  // Sumstat epilogue folded into this launch sequence (epi_tensors = [slab of all chunks,
+  // (LMODE 3); per_edge (the caller's choice when most groups are outside the EM range, e.g.
+  // a fit with narrow populations everywhere): LMODE 4, the per-edge kernel for every group
+  const bool em_resid = has_resid && !rel_tail && b.delta > 0.0f;
+  const bool ledge = per_edge && em_resid;
+  const bool lcall = !ledge && em_resid;
+  // Sumstat epilogue launched right after this forward (epi_tensors = [slab of all chunks,
   // target, S, loss, h, seq, err, advance] (empty = absent), epi_scalars = [rows before this
-  // chunk, eps, rank, timeout_s], epi_peers): the fix-up launch becomes one workgroup that
-  // ends with the epilogue, so a step has no separate epilogue launch; without a fix-up
-  // launch (no deferral) the epilogue kernel runs on its own.
+  // chunk, eps, rank, timeout_s], epi_peers): one host call per chunk instead of two.
   const bool with_epi = !epi_tensors.empty();
   EpiArgs epi{};
-  int64_t fixb = lmode ? (with_epi ? 1 : fix_blocks) : 0;
   if (with_epi) {
     TORCH_CHECK(epi_tensors.size() == 8 && epi_scalars.size() == 4, "epilogue: 8 tensors, 4 scalars");
     auto ptr_i = [](const torch::Tensor& t) -> int* {
@@ -2919,46 +2561,18 @@ int64_t smf_forward_lanes(torch::Tensor xi, torch::Tensor slot_pop, torch::Tenso
     };
     const int64_t row0 = (int64_t)epi_scalars[0];
     TORCH_CHECK(row0 >= 0, "bad row offset");
-    epi = make_epi(epi_tensors[0], row0 + nblocks + fixb, (int)scale.size(), nbp, epi_tensors[1],
+    epi = make_epi(epi_tensors[0], row0 + nblocks, (int)scale.size(), nbp, epi_tensors[1],
                    epi_scalars[1], epi_tensors[2], epi_tensors[3], epi_tensors[4], epi_peers,
                    (int64_t)epi_scalars[2], ptr_i(epi_tensors[5]), ptr_i(epi_tensors[6]),
                    epi_scalars[3], ptr_i(epi_tensors[7]));
     TORCH_CHECK(epi.slab + row0 * nbp == slab.data_ptr<float>(),
                 "the chunk's slab must start at the row offset of the full slab");
   }
-  // Folded epilogue (MG_FOLD_EPI, default off): without a fix-up launch the main launch
-  // runs the epilogue in its last workgroup to finish, counted on a self-resetting ticket
-  // (`defer` holds it then: one int32, zero between launches) -- one launch per step.
-  const bool fold = MG_FOLD_EPI && with_epi && !lmode && defer.has_value() && defer->defined();
-  int* tk = nullptr;
-  if (fold) {
-    check_dev(*defer, "ticket", at::kInt);
-    TORCH_CHECK(defer->numel() >= 1, "ticket: one int32");
-    tk = defer->data_ptr<int>();
-  }
-  const EpiArgs epi_main = fold ? epi : EpiArgs{};
-  int* dmain = lmode ? dp : tk;
-  auto fixup = [&]() {
-    if (!lmode) {
-      if (with_epi && !fold)
-        MG_DISPATCH_NB(nbp, {
-          hipLaunchKernelGGL((smf_epilogue_kernel<NB>), dim3(1), dim3(kEpiThreads), 0, stream, epi, b);
-        });
-      return;
-    }
-    if constexpr (kLanesMainMode == 1) {
-    float* fs = slab.data_ptr<float>() + nblocks * nbp;
-    MG_DISPATCH_NB(nbp, {
-      with_bool(log_sigma, [&](auto LS) {
-        hipLaunchKernelGGL((smf_fwd_lanes_kernel<NB, decltype(LS)::value, false, true, false, 2>),
-                           dim3(fixb), dim3(kThreads), 0, stream, xi.data_ptr<float>(),
-                           slot_pop.data_ptr<int32_t>(), group_base.data_ptr<int64_t>(),
-                           group_len.data_ptr<int32_t>(), fwd_order.data_ptr<int32_t>(), tp,
-                           (int64_t)0, (int64_t)0, b, fs, rp, nullptr, nullptr, 0, LanesUpdate{}, dp,
-                           epi);
+  auto epilogue = [&]() {
+    if (with_epi)
+      MG_DISPATCH_NB(nbp, {
+        hipLaunchKernelGGL((smf_epilogue_kernel<NB>), dim3(1), dim3(kEpiThreads), 0, stream, epi, b);
       });
-    });
-    }
   };
   if (update.has_value()) {
     // pipelined update: tensors [h, m, v, step(int32[2]), traj (or empty)] (+ [u, lo, hi]
@@ -3015,77 +2629,77 @@ int64_t smf_forward_lanes(torch::Tensor xi, torch::Tensor slot_pop, torch::Tenso
                              dim3(nblocks), dim3(kThreads), 0, stream, xi.data_ptr<float>(),
                              slot_pop.data_ptr<int32_t>(), group_base.data_ptr<int64_t>(),
                              group_len.data_ptr<int32_t>(), order, tp, g0, g1, b,
-                             slab.data_ptr<float>(), rp, ws, qp, nq, u, dmain, epi_main);
+                             slab.data_ptr<float>(), rp, ws, qp, nq, u);
         } else {
           hipLaunchKernelGGL((smf_fwd_lanes_kernel<NB, true, false, true, true, 4, true>),
                              dim3(nblocks), dim3(kThreads), 0, stream, xi.data_ptr<float>(),
                              slot_pop.data_ptr<int32_t>(), group_base.data_ptr<int64_t>(),
                              group_len.data_ptr<int32_t>(), order, tp, g0, g1, b,
-                             slab.data_ptr<float>(), rp, ws, qp, nq, u, tk, epi_main);
+                             slab.data_ptr<float>(), rp, ws, qp, nq, u);
         }
       });
-      fixup();
+      epilogue();
       if (u.host_step < 0 && !defer_advance)
         hipLaunchKernelGGL(smf_advance_step_kernel, dim3(1), dim3(1), 0, stream, U[3].data_ptr<int>());
-      return nblocks + fixb;
+      return nblocks;
     }
     MG_DISPATCH_NB(nbp, {
       with_bool(log_sigma, [&](auto LS) {
-        if (lmode || lcall) {
+        if (lcall) {
           hipLaunchKernelGGL((smf_fwd_lanes_kernel<NB, decltype(LS)::value, false, true, true, kLanesMainMode>),
                              dim3(nblocks), dim3(kThreads), 0, stream, xi.data_ptr<float>(),
                              slot_pop.data_ptr<int32_t>(), group_base.data_ptr<int64_t>(),
                              group_len.data_ptr<int32_t>(), order, tp, g0, g1, b,
-                             slab.data_ptr<float>(), rp, ws, qp, nq, u, dmain, epi_main);
+                             slab.data_ptr<float>(), rp, ws, qp, nq, u);
         } else if (ledge) {
           hipLaunchKernelGGL((smf_fwd_lanes_kernel<NB, decltype(LS)::value, false, true, true, 4>),
                              dim3(nblocks), dim3(kThreads), 0, stream, xi.data_ptr<float>(),
                              slot_pop.data_ptr<int32_t>(), group_base.data_ptr<int64_t>(),
                              group_len.data_ptr<int32_t>(), order, tp, g0, g1, b,
-                             slab.data_ptr<float>(), rp, ws, qp, nq, u, tk, epi_main);
+                             slab.data_ptr<float>(), rp, ws, qp, nq, u);
         } else {
           with_bool(rel_tail, [&](auto RT) {
             hipLaunchKernelGGL((smf_fwd_lanes_kernel<NB, decltype(LS)::value, decltype(RT)::value, true, true>),
                                dim3(nblocks), dim3(kThreads), 0, stream, xi.data_ptr<float>(),
                                slot_pop.data_ptr<int32_t>(), group_base.data_ptr<int64_t>(),
                                group_len.data_ptr<int32_t>(), order, tp, g0, g1, b,
-                               slab.data_ptr<float>(), rp, ws, qp, nq, u, tk, epi_main);
+                               slab.data_ptr<float>(), rp, ws, qp, nq, u);
           });
         }
       });
     });
-    fixup();  // after the update: the listed groups are evaluated at their new parameters
+    epilogue();
     if (u.host_step < 0 && !defer_advance)
       hipLaunchKernelGGL(smf_advance_step_kernel, dim3(1), dim3(1), 0, stream, U[3].data_ptr<int>());
-    return nblocks + fixb;
+    return nblocks;
   }
   MG_DISPATCH_NB(nbp, {
     with_bool(log_sigma, [&](auto LS) {
-      if (lmode || lcall) {
+      if (lcall) {
         hipLaunchKernelGGL((smf_fwd_lanes_kernel<NB, decltype(LS)::value, false, true, false, kLanesMainMode>),
                            dim3(nblocks), dim3(kThreads), 0, stream, xi.data_ptr<float>(),
                            slot_pop.data_ptr<int32_t>(), group_base.data_ptr<int64_t>(),
                            group_len.data_ptr<int32_t>(), order, tp, g0, g1, b,
-                           slab.data_ptr<float>(), rp, ws, qp, nq, LanesUpdate{}, dmain, epi_main);
+                           slab.data_ptr<float>(), rp, ws, qp, nq, LanesUpdate{});
       } else if (ledge) {
         hipLaunchKernelGGL((smf_fwd_lanes_kernel<NB, decltype(LS)::value, false, true, false, 4>),
                            dim3(nblocks), dim3(kThreads), 0, stream, xi.data_ptr<float>(),
                            slot_pop.data_ptr<int32_t>(), group_base.data_ptr<int64_t>(),
                            group_len.data_ptr<int32_t>(), order, tp, g0, g1, b,
-                           slab.data_ptr<float>(), rp, ws, qp, nq, LanesUpdate{}, tk, epi_main);
+                           slab.data_ptr<float>(), rp, ws, qp, nq, LanesUpdate{});
       } else {
         with_bool(rel_tail, [&](auto RT) { with_bool(has_resid, [&](auto RS) {
           hipLaunchKernelGGL((smf_fwd_lanes_kernel<NB, decltype(LS)::value, decltype(RT)::value, decltype(RS)::value>),
                              dim3(nblocks), dim3(kThreads), 0, stream, xi.data_ptr<float>(),
                              slot_pop.data_ptr<int32_t>(), group_base.data_ptr<int64_t>(),
                              group_len.data_ptr<int32_t>(), order, tp, g0, g1, b,
-                             slab.data_ptr<float>(), rp, ws, qp, nq, LanesUpdate{}, tk, epi_main);
+                             slab.data_ptr<float>(), rp, ws, qp, nq, LanesUpdate{});
         }); });
       }
     });
   });
-  fixup();
-  return nblocks + fixb;
+  epilogue();
+  return nblocks;
 }
 
 // Residual VJP over slots [s0, s1) plus the fixed-order finalize of split populations
@@ -3114,7 +2728,6 @@ void smf_vjp_lanes(torch::Tensor slot_pop, torch::Tensor slot_part, torch::Tenso
   TORCH_CHECK(s0 % kWave == 0 && s1 % kWave == 0, "slot ranges must be group aligned");
   TORCH_CHECK(resid.is_contiguous(), "resid must be contiguous");
   if (s1 > s0) {
-#if MG_VJP_LANES_PERSIST
     static int64_t caps[kMaxBins + 1] = {0};  // per padded bin count (register use differs)
     int64_t& cap = caps[nbp];
     if (cap == 0) {
@@ -3129,9 +2742,6 @@ void smf_vjp_lanes(torch::Tensor slot_pop, torch::Tensor slot_part, torch::Tenso
     }
     const int64_t want = (s1 - s0 + kThreads - 1) / kThreads;
     const int64_t nblk = std::max<int64_t>(kXcds, std::min(cap, want) / kXcds * kXcds);
-#else
-    const int64_t nblk = (s1 - s0 + kThreads - 1) / kThreads;
-#endif
     MG_DISPATCH_NB(nbp, {
       with_bool(log_sigma, [&](auto LS) {
         hipLaunchKernelGGL((smf_vjp_lanes_kernel<NB, decltype(LS)::value>), dim3(nblk), dim3(kThreads), 0,

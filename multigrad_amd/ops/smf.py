@@ -383,31 +383,12 @@ class PopulationShard:
             self.resid = torch.empty(shape, dtype=torch.float32, device=self.device)
         return self.resid
 
-    def defer_buffer(self) -> torch.Tensor:
-        """Device list of the residual lanes forwards ([count, ticket, one slot per group]):
-        groups outside the Euler-Maclaurin range are deferred by the main launch to a
-        fix-up launch of LANES_FIX_BLOCKS workgroups (csrc/smf.hip, LMODE).  Both counters
-        are left at 0 by the fix-up launch itself."""
-        if getattr(self, "_defer", None) is None or self._defer.numel() < 2 + self.ngroups:
-            self._defer = torch.zeros(2 + self.ngroups, dtype=torch.int32, device=self.device)
-        return self._defer
-
-    def fold_ticket(self) -> torch.Tensor:
-        """One int32 on the device, zero between launches: the workgroup-completion ticket
-        of a lanes forward that runs the sumstat epilogue in its last workgroup (csrc/smf.hip,
-        MG_FOLD_EPI; the launch resets it)."""
-        if getattr(self, "_ticket", None) is None:
-            self._ticket = torch.zeros(1, dtype=torch.int32, device=self.device)
-        return self._ticket
-
     def fwd_rows(self, nhalos: int, nbins: int = 10, log_sigma: bool = True,
                  rel_tail: bool = False, chunk: Optional[int] = None, resid: bool = True) -> int:
-        """Slab rows a forward over ``chunk`` writes: the forward grid (:meth:`fwd_blocks`)
-        plus, for residual forwards of the lanes layout, the fix-up launch's rows."""
-        n = self.fwd_blocks(nhalos, nbins, log_sigma, rel_tail, chunk)
-        if self.device.type == "cuda" and self.layout == "lanes" and resid:
-            n += lanes_fix_blocks()
-        return n
+        """Slab rows a forward over ``chunk`` writes: one per workgroup of the forward grid
+        (:meth:`fwd_blocks`).  ``resid`` is accepted for the engine interface; the residual
+        forwards have no extra rows since the deferral list's fix-up launch was removed."""
+        return self.fwd_blocks(nhalos, nbins, log_sigma, rel_tail, chunk)
 
     @property
     def vjp_recompute(self) -> bool:
@@ -460,14 +441,6 @@ class PopulationShard:
 
 
 _GRID_CACHE: dict = {}
-# workgroups of the fix-up launch that evaluates the groups a residual lanes forward deferred
-# (outside the Euler-Maclaurin range) in builds with -DMG_LANES_DEFER=1 (round 3).  An empty
-# fix-up launch of 64 workgroups measured 16.5 us, of 1 workgroup 7.4 us (the count read and
-# the reset are memory round trips; the 64 tickets serialise).  The default build
-# (MG_LANES_DEFER 2) evaluates those groups inside the main launch and has no fix-up rows.
-LANES_FIX_BLOCKS = int(os.environ.get("MULTIGRAD_FIX_BLOCKS", "8"))
-
-
 # Share of per-edge lane groups (narrow populations, PopulationShard.per_edge_share) from
 # which the residual lanes forward runs the per-edge kernel for every group (LMODE 4)
 # instead of the Euler-Maclaurin kernel with its out-of-line per-edge call: measured on one
@@ -475,15 +448,6 @@ LANES_FIX_BLOCKS = int(os.environ.get("MULTIGRAD_FIX_BLOCKS", "8"))
 # 446 + 410 f us at a per-edge share f and the per-edge kernel 617-627 us, so they cross
 # near f = 0.42.
 PER_EDGE_SHARE = float(os.environ.get("MULTIGRAD_PER_EDGE_SHARE", "0.45"))
-
-
-def lanes_fix_blocks() -> int:
-    """Slab rows of the fix-up launch of a residual lanes forward: LANES_FIX_BLOCKS when
-    the extension runs the deferral list (MG_LANES_DEFER 1), else 0."""
-    if "fix" not in _GRID_CACHE:
-        fn = getattr(ext(), "smf_lanes_fallback_mode", None)
-        _GRID_CACHE["fix"] = LANES_FIX_BLOCKS if fn is None or int(fn()) == 1 else 0
-    return _GRID_CACHE["fix"]
 
 
 def _sort_by_population(pop_cpu: torch.Tensor, npop: int):
@@ -593,7 +557,7 @@ def smf_forward_slab(theta: torch.Tensor, shard: PopulationShard, bins: SmfBins,
                 upd += [u["u"], u["lo"], u["hi"]]
                 usc.append(float(bool(u.get("legacy", False))))
         et, es, ep = [], [], []
-        if epilogue is not None:  # the sumstat epilogue folded into this launch sequence
+        if epilogue is not None:  # the sumstat epilogue launched by the same host call
             e = epilogue
             none = torch.empty(0, dtype=torch.int32, device=theta.device)
             os_ = e.get("oneshot")
@@ -608,9 +572,7 @@ def smf_forward_slab(theta: torch.Tensor, shard: PopulationShard, bins: SmfBins,
                                        shard.group_len, shard.fwd_order, theta, list(bins.edges),
                                        list(bins.scale), bool(log_sigma), g0, g1, slab, nblk,
                                        bins.rel_tail, rbuf, w_order, w_start, queues, upd, usc,
-                                       shard.defer_buffer() if resid and lanes_fix_blocks()
-                                       else shard.fold_ticket() if epilogue is not None else None,
-                                       lanes_fix_blocks() if resid else 0, et, es, ep,
+                                       et, es, ep,
                                        bool(resid and shard.per_edge_share(chunk) >= PER_EDGE_SHARE))
         if resid:
             shard.resid_epoch += 1

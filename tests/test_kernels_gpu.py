@@ -391,11 +391,10 @@ def test_fused_epilogue_matches_separate_kernels(graph):
 
 @pytest.mark.parametrize("narrow", [False, True])
 def test_folded_epilogue_matches_separate_launch(monkeypatch, narrow):
-    """The sumstat epilogue passed to the forward's launch sequence
-    (MULTIGRAD_FOLD_EPILOGUE: with the default MG_LANES_DEFER 2 build the forward launches
-    it right after the main kernel; with -DMG_LANES_DEFER=1 it rides on the fix-up launch)
-    against the engine's own epilogue launch, pipelined, with no narrow population and
-    with narrow populations on the per-edge path; the deferral list stays at zero."""
+    """The sumstat epilogue passed to the forward's host call (MULTIGRAD_FOLD_EPILOGUE: the
+    forward launches it right after the main kernel) against the engine's own epilogue
+    launch, pipelined, with no narrow population and with narrow populations on the
+    per-edge path."""
     from multigrad_amd.engine.fused import FusedAdamEngine
     from multigrad_amd.models.population import PopulationSMFModel, make_population_data
     data = make_population_data(num_params=6000, num_halos=300_000, seed=21, device=DEV)
@@ -408,15 +407,10 @@ def test_folded_epilogue_matches_separate_launch(monkeypatch, narrow):
         eng = FusedAdamEngine(model, graph=False)
         out[fold] = (eng.run_adam(guess, nsteps=5, learning_rate=1e-3), eng.loss.clone(), eng.h.clone())
         assert eng.pipeline
-        assert int(data["shard"].defer_buffer()[:2].abs().sum()) == 0
-    torch.testing.assert_close(out["1"][0], out["0"][0], rtol=1e-6, atol=1e-7)
-    # the two schedules reduce different numbers of slab rows (1 fix-up row vs
-    # MULTIGRAD_FIX_BLOCKS), so the float sums differ in order
-    torch.testing.assert_close(out["1"][1], out["0"][1], rtol=1e-5, atol=0)
-    # h: differences of cotangent terms, so an ulp of S (the slab rows are grouped
-    # differently per thread: one fix-up row instead of eight) shows up at ~1e-6 relative
-    torch.testing.assert_close(out["1"][2], out["0"][2], rtol=1e-5,
-                               atol=1e-6 * float(out["0"][2].abs().max()))
+    # the same kernels over the same slab rows in the same order: the same bits
+    torch.testing.assert_close(out["1"][0], out["0"][0], rtol=0, atol=0)
+    torch.testing.assert_close(out["1"][1], out["0"][1], rtol=0, atol=0)
+    torch.testing.assert_close(out["1"][2], out["0"][2], rtol=0, atol=0)
 
 
 @pytest.mark.parametrize("owner,graph,legacy,kind", [
@@ -599,9 +593,7 @@ def test_em_forward_fallback_groups_vs_fp64():
     th = _narrow_guess(data)
     out = torch.zeros(bins.nbp, device=DEV)
     S.smf_forward_into(th, shard, bins, True, out, resid=True)
-    # the narrow groups went through the out-of-line per-edge call (default build) or the
-    # deferral list and fix-up launch (-DMG_LANES_DEFER=1), which leaves the counters at 0
-    assert int(shard.defer_buffer()[:2].abs().sum()) == 0
+    # (the narrow groups went through the out-of-line per-edge call, LMODE 3)
     ref = S.smf_sumstats_reference(th.double(), shard.x.double(), shard.pop, bins, True)
     np.testing.assert_allclose(out[:bins.nb].cpu().double(), ref.cpu(), rtol=2e-5)
     h = torch.linspace(0.6, -0.5, bins.nbp + 1, device=DEV)
