@@ -117,22 +117,12 @@ __device__ __forceinline__ void normal_tail_parts_w(float w, float& p, float& g)
 // normal_tail_parts_w.
 typedef float v2f __attribute__((ext_vector_type(2)));
 
-// PAIR_RCP: the two reciprocals share one v_rcp (1/a = b/(ab), 1/b = a/(ab)); both
-// factors are >= K, so ab only overflows for the lane sentinel (|w| ~ 1e30), where the
-// reciprocal becomes 0 and the Gaussian factor 0 keeps the contribution exactly zero.
-#ifndef MG_PAIR_RCP
-#define MG_PAIR_RCP 0
-#endif
+// The two reciprocals of a pair, one v_rcp each.  (Sharing one v_rcp, 1/a = b/(ab), was a
+// compiled-out variant until round 5, when the unmeasured switch was removed.)
 __device__ __forceinline__ v2f pair_rcp(float a, float b) {
   v2f r;
-#if MG_PAIR_RCP
-  const float R = fast_rcp(a * b);
-  r.x = R * b;
-  r.y = R * a;
-#else
   r.x = fast_rcp(a);
   r.y = fast_rcp(b);
-#endif
   return r;
 }
 

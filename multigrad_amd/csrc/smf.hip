@@ -153,9 +153,12 @@ __device__ __forceinline__ void halo_mass(float x, float2 th, const SmfBins& b,
   }
 }
 
-// Forward tunables (halos per thread per iteration; minimum resident waves per SIMD).
+// Tiles-forward tunables (halos per thread per iteration; minimum resident waves per SIMD).
+// Same-box A/B on the hashed per-rank proxy (1e7 params, 1/8 of the halos, ms/step, three
+// alternating runs, profiles/fwd_knobs_r5/): unroll 1 0.1638-0.1665 vs 2 0.1668-0.1675;
+// unroll 4 0.2901-0.2921 (spills); 6 waves 0.1659-0.1683 vs 8 0.1667-0.1691 (a tie).
 #ifndef MG_FWD_UNROLL
-#define MG_FWD_UNROLL 2
+#define MG_FWD_UNROLL 1
 #endif
 #ifndef MG_FWD_MINWAVES
 #define MG_FWD_MINWAVES 8
@@ -515,7 +518,10 @@ __device__ __forceinline__ int8_t bound_kind(float lo, float hi) {
 // instead of IEEE divisions (~10 VALU ops each, three per coordinate): the update runs in the
 // VALU-bound forward, where they measured 480 vs 440 us per step (the stand-alone bounded
 // Adam keeps the exact forms; the two schedules agree to a few ulps, as the unbounded
-// pipelined update's reciprocal bias corrections do)
+// pipelined update's reciprocal bias corrections do).  What the bounded update costs
+// (profiles/bounded_r5/): 1.72e8 vs 1.63e8 VALU wave instructions per step, ~115 per lane
+// group, a third of them SGPR spill traffic (v_readlane / v_writelane) around the group
+// transition; a wave-uniform fast path for all-both-bounded waves measured no faster.
 __device__ __forceinline__ float dpdu_fast(float at, float lo, float hi, int8_t k) {
   if (k == kBoth) {
     const float r = at * __builtin_amdgcn_rcpf((hi - lo) * (1.0f / kPi));
