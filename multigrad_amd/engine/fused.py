@@ -1126,8 +1126,8 @@ class FusedAdamEngine:
         fused_ok = (fused is not None and self.fuse_epilogue
                     and (self.size == 1 or self.oneshot is not None) and self.slab.is_cuda)
         advance = None
-        # the epilogue can ride on the last chunk's forward launches (one launch per step
-        # fewer; ops/smf.py, csrc/smf.hip LMODE 2 + epilogue_block)
+        # the last chunk's forward host call also issues the epilogue launch (one host call
+        # per step fewer; ops/smf.py:smf_forward_into, csrc/smf.hip:smf_forward_lanes)
         fold = fused_ok and _env_flag("MULTIGRAD_FOLD_EPILOGUE", True) and \
             getattr(md, "engine_forward_epilogue_ok", lambda: False)()
         chunks = [self.rank] if self.owner else list(range(self.C))
