@@ -57,6 +57,7 @@ from __future__ import annotations
 
 import math
 import os
+import weakref
 from typing import Optional
 
 import torch
@@ -67,6 +68,17 @@ from ..optim.adam import History
 from ..optim.transforms import Bounds
 from ..utils.random import PRNGKey, init_randkey
 from ..utils.tensors import as_param_tensor
+
+
+def _give_back_ar(ts, pins) -> None:
+    """Finalizer of an engine's hold on a two-shot all-reduce context: the hold and the
+    pins of the engine's captured graphs (``pins``: a one-element list, updated by the
+    engine as it captures)."""
+    from ..parallel.xgmi import release_twoshot_allreduce, unpin_twoshot_allreduce
+    unpin_twoshot_allreduce(ts, pins[0])
+    pins[0] = 0
+    release_twoshot_allreduce(ts)
+
 
 __all__ = ["GraphAdamEngine", "KeyNotCapturable"]
 
@@ -270,6 +282,11 @@ class GraphAdamEngine:
                 P_pad = -(-P // q) * q
                 if sgd:  # the summed gradient itself is needed: a capturable all-reduce
                     self.ar = get_twoshot_allreduce(self.comm, P, hold=True)
+                    # the hold and the pins of this engine's graphs go back to the
+                    # communicator's cache at close() -- or when the engine is dropped
+                    # without it (the finalizer holds no reference to the engine)
+                    self._ar_pins = [0]
+                    self._ar_fin = weakref.finalize(self, _give_back_ar, self.ar, self._ar_pins)
                 else:
                     self.twoshot = acquire_twoshot(self.comm, P_pad) if twoshot_enabled() else None
                 if self.group:
@@ -372,13 +389,19 @@ class GraphAdamEngine:
     @on_engine_stream
     def close(self) -> None:
         """Give the two-shot context back to the communicator's pool (collective: every
-        rank closes its engine the same way); setup() calls it before re-connecting."""
+        rank closes its engine the same way); setup() calls it before re-connecting.  Graphs
+        that recorded exchanges on the all-reduce context are dropped with it (their pins go
+        back with the hold)."""
+        if self.ar is not None and getattr(self, "_ar_pins", [0])[0]:
+            self.graph = None
+            self._kgraph = None
         if self.twoshot is not None:
             from ..parallel.xgmi import release_twoshot
             release_twoshot(self.comm, self.twoshot)
-        if self.ar is not None:
-            from ..parallel.xgmi import release_twoshot_allreduce
-            release_twoshot_allreduce(self.ar)
+        fin = getattr(self, "_ar_fin", None)
+        if fin is not None:
+            fin()  # release the hold and this engine's pins (once)
+            self._ar_fin = None
         self.twoshot = None
         self.ar = None
         self.ready = False
@@ -580,10 +603,21 @@ class GraphAdamEngine:
         graph = torch.cuda.CUDAGraph()
         for gen in self._gens:
             graph.register_generator_state(gen)
+        pins = self._ar_pin_count()
         with _no_gc():
             with torch.cuda.graph(graph):
                 self._body(None, key)
+        self._ar_note_pins(pins)
         return graph
+
+    def _ar_pin_count(self) -> int:
+        return self.ar.pins if self.ar is not None else 0
+
+    def _ar_note_pins(self, before: int) -> None:
+        """Account the exchanges a capture recorded on the all-reduce context (pins held
+        until close())."""
+        if self.ar is not None:
+            self._ar_pins[0] += self.ar.pins - before
 
     def _replay(self, key) -> None:
         """Replay the captured step (on the engine stream, like every launch of the engine:
@@ -615,10 +649,12 @@ class GraphAdamEngine:
         """Capture ``k`` steps into one graph (after the one-step capture, which warmed up
         the allocator and the kernels); each step reads and advances the device step."""
         g = torch.cuda.CUDAGraph()
+        pins = self._ar_pin_count()
         with _no_gc():
             with torch.cuda.graph(g):
                 for _ in range(int(k)):
                     self._body(None, None)
+        self._ar_note_pins(pins)
         return g
 
     @on_engine_stream

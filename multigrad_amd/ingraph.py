@@ -97,6 +97,7 @@ def simple_grad_descent(data_dict, loss_and_grad_func: Callable, guess, learning
         step.add_(1)
 
     done = False
+    pins0 = ts.pins if ts is not None else 0
     if use_graph and n > 0:
         saved = params.clone()
         # whole-loop capture in blocks: one graph of K unrolled steps replayed n // K times,
@@ -141,7 +142,11 @@ def simple_grad_descent(data_dict, loss_and_grad_func: Callable, guess, learning
                 body()
                 if hooks.active:
                     hooks(i, losses[i], None, lambda: params)
+    if use_graph and n > 0:
+        del graphs  # the exchanges they recorded no longer pin the cached context
     if ts is not None:
+        from .parallel.xgmi import unpin_twoshot_allreduce
+        unpin_twoshot_allreduce(ts, ts.pins - pins0)
         ts.check("ingraph.simple_grad_descent", comm)  # a timed-out exchange raises here
     loss_np = losses.detach().cpu().numpy()
     par_np = hist.detach().cpu().numpy()

@@ -429,7 +429,9 @@ class TwoShot:
         # between calls, and graphs captured around it (pinned: a replay may come any time);
         # the cache evicts only contexts that nobody holds
         self.holders = 0
-        self.pinned = False
+        # exchanges recorded into graphs that may still be replayed; the capturer gives them
+        # back with unpin() when it drops its graphs (generic engine close(), ingraph's loop)
+        self.pins = 0
 
     def _blocks(self, max_blocks: int) -> int:
         mb = int(max_blocks)
@@ -509,7 +511,7 @@ class TwoShot:
                              f"{self.numel} elements expected, got {t.dtype} x {k}")
         flat = t.view(-1)
         if torch.cuda.is_current_stream_capturing():
-            self.pinned = True  # a replay of this graph may come at any time: never evict
+            self.pins += 1  # a replay of this graph may come at any time: never evict
         self.grad[:k].copy_(flat)
         lo, n = self.slice()
         self.step(lo, n, 0)
@@ -597,9 +599,10 @@ def get_twoshot_allreduce(comm, numel: int, hold: bool = False) -> Optional[TwoS
     ``_MAX_AR_CONTEXTS`` working contexts that nobody uses are kept; connecting a larger one
     closes the smallest of those (every rank makes the same calls in the same order, so the
     caches agree).  A context is in use while a caller holds it (``hold=True``, given back
-    with :func:`release_twoshot_allreduce`) or once a graph captured an exchange on it
-    (pinned for the communicator's lifetime: the graph may be replayed at any time); a
-    closed context raises on use instead of touching unmapped peer memory."""
+    with :func:`release_twoshot_allreduce`) or while a graph that captured an exchange on it
+    may still be replayed (``pins``, given back with :func:`unpin_twoshot_allreduce` by the
+    capturer when it drops the graph); a closed context raises on use instead of touching
+    unmapped peer memory."""
     if (comm is None or comm.size < 2 or comm.size > MAX_RANKS or not twoshot_enabled()
             or not torch.cuda.is_available()):
         return None
@@ -624,7 +627,7 @@ def get_twoshot_allreduce(comm, numel: int, hold: bool = False) -> Optional[TwoS
     cache[want] = ts
     if ts:
         ts.holders += int(hold)
-    idle = sorted(have for have, t in cache.items() if t and not t.holders and not t.pinned)
+    idle = sorted(have for have, t in cache.items() if t and not t.holders and not t.pins)
     while len(idle) > _MAX_AR_CONTEXTS:
         torch.cuda.synchronize()
         comm.barrier()
@@ -667,6 +670,12 @@ def release_twoshot_allreduce(ts: Optional[TwoShot]) -> None:
     """Give back a context taken with ``get_twoshot_allreduce(..., hold=True)``."""
     if ts:
         ts.holders = max(0, ts.holders - 1)
+
+
+def unpin_twoshot_allreduce(ts: Optional[TwoShot], n: int) -> None:
+    """Give back ``n`` pins (exchanges captured into graphs the caller has dropped)."""
+    if ts:
+        ts.pins = max(0, ts.pins - int(n))
 
 
 def acquire_twoshot(comm, numel: int) -> Optional[TwoShot]:

@@ -472,3 +472,39 @@ def test_direct_steps_with_default_stream_work_match_eager(engine):
         torch.cuda.synchronize()
     got = eng.trajectory().cpu()
     torch.testing.assert_close(got, want, rtol=1e-6, atol=1e-7)
+
+
+def _ar_give_back(rank, size):
+    import gc
+
+    import multigrad_amd as mg
+    from multigrad_amd.engine.generic import GraphAdamEngine
+    comm = mg.get_world_comm()
+    m, guess = _torch_pop(comm=comm, npar=2000, nhalo=40_000)
+    # run_simple_grad_descent closes its engine: hold and pins given back
+    eng = GraphAdamEngine(m)
+    eng.run_simple_grad_descent(guess, nsteps=6, learning_rate=3e-3)
+    ar = comm._twoshot_ar[min(comm._twoshot_ar)]
+    after_run = (ar.holders, ar.pins)
+    # an engine dropped without close(): the finalizer gives them back
+    eng = GraphAdamEngine(m)
+    eng.mode = "sgd"
+    eng.setup(guess, 6, learning_rate=3e-3, history="last")
+    eng.steps(6)
+    torch.cuda.synchronize()
+    during = (eng.ar.holders, eng.ar.pins, eng.use_graph)
+    ar = eng.ar
+    del eng
+    gc.collect()
+    return after_run, during, (ar.holders, ar.pins)
+
+
+def test_allreduce_context_hold_and_pins_given_back():
+    """the generic engine's hold on its two-shot all-reduce context and
+    the pins of its captured graphs go back to the communicator's cache on close() and
+    when the engine is dropped without it, so the cache can evict the context again."""
+    res = run_distributed(_ar_give_back, 2, timeout=300)
+    for after_run, during, dropped in res:
+        assert after_run == (0, 0)
+        assert during[0] == 1 and during[2] and during[1] >= 1
+        assert dropped == (0, 0)
