@@ -168,16 +168,20 @@ constexpr int kFwdUnroll = MG_FWD_UNROLL;
 // XS (fused exchange): workgroups [0, xs.blocks) run the two-shot exchange of the previous
 // parameter chunk (twoshot.h) and the rest this forward, with their own block numbering --
 // the exchange overlaps the forward without a second stream or cross-stream events.
-template <int NB, bool LOGSIG, bool HAS_POP, bool REL, bool XS = false>
-__global__ __launch_bounds__(kThreads, MG_FWD_MINWAVES) void smf_fwd_kernel(
+// XS = 1: unbounded Adam (mode 1); 2: bounded (modes 2 / 3, its own instantiation so the
+// unbounded kernel keeps its registers; 6 waves per SIMD instead of 8, which measured the
+// same for this kernel, leave the bounded Adam 80 VGPRs instead of spilling at 64).
+template <int NB, bool LOGSIG, bool HAS_POP, bool REL, int XS = 0>
+__global__ __launch_bounds__(kThreads, XS == 2 ? 6 : MG_FWD_MINWAVES) void smf_fwd_kernel(
     const float* __restrict__ x, const int32_t* __restrict__ pop,
     const float2* __restrict__ theta, int64_t begin, int64_t end, SmfBins bins,
     float* __restrict__ slab, TwoShotPack xs = TwoShotPack{}) {
   int bid = blockIdx.x, nblk = gridDim.x;
-  if constexpr (XS) {
+  if constexpr (XS > 0) {
     if (bid < xs.blocks) {
       __shared__ int xs_lds[2];  // 8 bytes: this kernel's occupancy is set by its VGPRs
-      twoshot_block_fused(xs.a, bid, xs.blocks, xs_lds);
+      if constexpr (XS == 2) twoshot_block_fused_bounded(xs.a, xs.mode, bid, xs.blocks, xs_lds);
+      else twoshot_block_fused(xs.a, bid, xs.blocks, xs_lds);
       return;
     }
     bid -= xs.blocks;
@@ -1160,11 +1164,11 @@ __device__ __forceinline__ void halo_vjp_rec(float nm, float inv, float dw, cons
   wc = ws.x;
 }
 
-template <int NB, bool LOGSIG, bool XS = false>
+template <int NB, bool LOGSIG, int XS = 0>
 #ifndef MG_VJP_REC_MINWAVES
 #define MG_VJP_REC_MINWAVES 8  // 20 KB of LDS and <= 64 VGPRs: 8 workgroups per CU
 #endif
-__global__ __launch_bounds__(kThreads, MG_VJP_REC_MINWAVES) void smf_vjp_tiles_rec_kernel(
+__global__ __launch_bounds__(kThreads, XS == 2 ? 6 : MG_VJP_REC_MINWAVES) void smf_vjp_tiles_rec_kernel(
     const float* __restrict__ x, const int32_t* __restrict__ pop,
     const float2* __restrict__ theta, const Tile* __restrict__ tiles,
     const float* __restrict__ hvec, SmfBins bins, float2* __restrict__ grad,
@@ -1178,9 +1182,12 @@ __global__ __launch_bounds__(kThreads, MG_VJP_REC_MINWAVES) void smf_vjp_tiles_r
   // fused kernel keeps the same 20 KB and 8 workgroups per CU
   __shared__ __attribute__((aligned(16))) char smem[kTileHalos * (sizeof(float2) + sizeof(int16_t))];
   int tb = blockIdx.x;
-  if constexpr (XS) {
+  if constexpr (XS > 0) {
     if (tb < xs.blocks) {
-      twoshot_block_fused(xs.a, tb, xs.blocks, reinterpret_cast<int*>(smem));
+      if constexpr (XS == 2)
+        twoshot_block_fused_bounded(xs.a, xs.mode, tb, xs.blocks, reinterpret_cast<int*>(smem));
+      else
+        twoshot_block_fused(xs.a, tb, xs.blocks, reinterpret_cast<int*>(smem));
       return;
     }
     tb -= xs.blocks;
@@ -2158,13 +2165,18 @@ void smf_forward(torch::Tensor x, c10::optional<torch::Tensor> pop, torch::Tenso
   float* sp = slab.data_ptr<float>();
   if (!exchange.empty()) {
     const TwoShotPack xs = twoshot_unpack(exchange);
-    if (has_pop && !rel_tail && xs.mode == 1) {
+    if (has_pop && !rel_tail && xs.mode >= 1 && xs.mode <= 3) {
       TORCH_CHECK(nblocks + xs.blocks <= 65535, "bad block count");
       MG_DISPATCH_NB(nbp, {
         with_bool(log_sigma, [&](auto LS) {
-          hipLaunchKernelGGL((smf_fwd_kernel<NB, decltype(LS)::value, true, false, true>),
-                             dim3(nblocks + xs.blocks), dim3(kThreads), 0, stream, xp, pp, tp, begin,
-                             end, b, sp, xs);
+          if (xs.mode == 1)
+            hipLaunchKernelGGL((smf_fwd_kernel<NB, decltype(LS)::value, true, false, 1>),
+                               dim3(nblocks + xs.blocks), dim3(kThreads), 0, stream, xp, pp, tp,
+                               begin, end, b, sp, xs);
+          else
+            hipLaunchKernelGGL((smf_fwd_kernel<NB, decltype(LS)::value, true, false, 2>),
+                               dim3(nblocks + xs.blocks), dim3(kThreads), 0, stream, xp, pp, tp,
+                               begin, end, b, sp, xs);
         });
       });
       return;
@@ -2326,13 +2338,22 @@ void smf_vjp(torch::Tensor x, c10::optional<torch::Tensor> pop, torch::Tensor th
   bool fused = false;
   if (!exchange.empty()) {
     const TwoShotPack xs = twoshot_unpack(exchange);
-    if (rec && xs.mode == 1) {
+    if (rec && xs.mode >= 1 && xs.mode <= 3) {
       TORCH_CHECK(ntiles + xs.blocks <= INT32_MAX, "bad block count");
+      const dim3 grid(ntiles + xs.blocks);
+      const float* hp = h.data_ptr<float>();
       MG_DISPATCH_NB(nbp, {
-        if (log_sigma)
-          hipLaunchKernelGGL((smf_vjp_tiles_rec_kernel<NB, true, true>), dim3(ntiles + xs.blocks), dim3(kThreads), 0, stream, xp, pp, tp, tl, h.data_ptr<float>(), b, gp, pa, xs);
-        else
-          hipLaunchKernelGGL((smf_vjp_tiles_rec_kernel<NB, false, true>), dim3(ntiles + xs.blocks), dim3(kThreads), 0, stream, xp, pp, tp, tl, h.data_ptr<float>(), b, gp, pa, xs);
+        if (xs.mode == 1) {
+          if (log_sigma)
+            hipLaunchKernelGGL((smf_vjp_tiles_rec_kernel<NB, true, 1>), grid, dim3(kThreads), 0, stream, xp, pp, tp, tl, hp, b, gp, pa, xs);
+          else
+            hipLaunchKernelGGL((smf_vjp_tiles_rec_kernel<NB, false, 1>), grid, dim3(kThreads), 0, stream, xp, pp, tp, tl, hp, b, gp, pa, xs);
+        } else {
+          if (log_sigma)
+            hipLaunchKernelGGL((smf_vjp_tiles_rec_kernel<NB, true, 2>), grid, dim3(kThreads), 0, stream, xp, pp, tp, tl, hp, b, gp, pa, xs);
+          else
+            hipLaunchKernelGGL((smf_vjp_tiles_rec_kernel<NB, false, 2>), grid, dim3(kThreads), 0, stream, xp, pp, tp, tl, hp, b, gp, pa, xs);
+        }
       });
       fused = true;
     } else {

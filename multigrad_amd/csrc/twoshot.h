@@ -50,7 +50,10 @@ constexpr int kTsThreads = 256;
 // workgroup's share is done (the last one returns when every rank's slice has landed).
 // `lds`: two ints of LDS for the block-wide flags (lent by the caller: the fused VJP sits at
 // exactly 20 KiB so that 8 workgroups fit a CU, and a __shared__ here would add to it).
-template <int MODE, int PB = kXMaxRanks>
+// LEAN: one element's Adam at a time (scalar loads of its state, scheduling barriers
+// between the four), for the bounded modes carried by compute kernels whose launch bounds
+// allow 64 VGPRs (the float4 form spilled 43-65 VGPRs there).
+template <int MODE, int PB = kXMaxRanks, bool LEAN = false>
 __device__ __forceinline__ void twoshot_block(const TwoShotArgs& a, int bid, int nblk, int* lds) {
   static_assert(kXMaxRanks % PB == 0, "peer batches must tile the rank limit");
   static_assert(MODE >= 0 && MODE <= 5, "two-shot mode");
@@ -103,7 +106,34 @@ __device__ __forceinline__ void twoshot_block(const TwoShotArgs& a, int bid, int
       g = reinterpret_cast<const float4*>(a.u)[i];
     }
     float4 p = g;
-    if constexpr (ADAM) {
+    if constexpr (ADAM && LEAN) {
+      // one element at a time: scalar loads of its state, a scheduling barrier after each
+      const float gs[4] = {g.x, g.y, g.z, g.w};
+      float ps[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int64_t e = 4 * i + q;
+        float uu = BOUNDED ? a.u[e] : own[e];
+        float mm = a.m[e], vv = a.v[e], po = 0.f, lo = 0.f, hi = 0.f;
+        int8_t kk = 0;
+        if constexpr (BOUNDED) {
+          lo = a.blo[e];
+          hi = a.bhi[e];
+          kk = a.kind[e];
+          if (LEGACY) po = own[e];
+        }
+        float pp;
+        adam_elem<BOUNDED, LEGACY>(a, bc1, bc2, gs[q], uu, mm, vv, po, lo, hi, kk, pp);
+        if (bad) uu = pp = __builtin_nanf("");
+        a.m[e] = mm;
+        a.v[e] = vv;
+        if constexpr (BOUNDED) a.u[e] = uu;
+        if (trow) trow[e] = pp;
+        ps[q] = pp;
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      p = make_float4(ps[0], ps[1], ps[2], ps[3]);
+    } else if constexpr (ADAM) {
       float4 u = BOUNDED ? reinterpret_cast<const float4*>(a.u)[i]
                          : reinterpret_cast<const float4*>(own)[i];
       float4 m = reinterpret_cast<const float4*>(a.m)[i];
@@ -161,11 +191,17 @@ __device__ __forceinline__ void twoshot_block(const TwoShotArgs& a, int bid, int
 }
 
 
-// The exchange carried by a compute kernel (fused exchange): unbounded Adam only (the
-// bounded modes launch on their own, see smf_forward / smf_vjp), peers 4 at a time.
+// The exchange carried by a compute kernel (fused exchange), peers 4 at a time: unbounded
+// Adam (mode 1), or bounded (mode 2, or 3 with the legacy Jacobian) in the kernels' separate
+// bounded instantiations (XS = 2 in smf.hip), so the unbounded ones keep their registers.
 __device__ __forceinline__ void twoshot_block_fused(const TwoShotArgs& a, int bid, int nblk,
                                                     int* lds) {
   twoshot_block<1, 4>(a, bid, nblk, lds);
+}
+__device__ __forceinline__ void twoshot_block_fused_bounded(const TwoShotArgs& a, int mode,
+                                                            int bid, int nblk, int* lds) {
+  if (mode == 3) twoshot_block<3, 4, true>(a, bid, nblk, lds);
+  else twoshot_block<2, 4, true>(a, bid, nblk, lds);
 }
 
 // Packed launch arguments of one exchange (xgmi_twoshot_pack -> the fused kernels' host

@@ -462,13 +462,13 @@ class FusedAdamEngine:
         # fused exchange ("ts_fused"): the two-shot exchange of chunk c-1 runs in the first
         # workgroups of chunk c's VJP launch and the last chunk's in the next step's first
         # forward launch (csrc/twoshot.h) -- overlap with compute on ONE stream, no events.
-        # Unbounded fits with >= 2 chunks on a model whose kernels carry it.
+        # >= 2 chunks on a model whose kernels carry it (bounded fits: modes 2 / 3).
         # MULTIGRAD_TWOSHOT_FUSED: auto (an autotune candidate), on (always, no tuning), off
         self._x_pending = None  # packed exchange of the last chunk, for the next launch
         fmode = os.environ.get("MULTIGRAD_TWOSHOT_FUSED", "auto").strip().lower()
         self.ts_fused_ok = bool(
             fmode not in ("0", "off", "false", "no") and self.twoshot is not None
-            and self.C > 1 and bounds is None
+            and self.C > 1
             and getattr(md, "engine_fused_exchange_ok", lambda: False)())
         self.ts_fused = self.ts_fused_ok and fmode in ("1", "on", "true", "yes")
         if self.ts_fused:
@@ -929,16 +929,21 @@ class FusedAdamEngine:
         self.ready = False
 
     def _ts_pack(self, c: int) -> bytes:
-        """Chunk c's two-shot exchange (reduce-scatter -> unbounded Adam -> all-gather) as
-        packed launch arguments for a compute launch that carries it (fused exchange)."""
+        """Chunk c's two-shot exchange (reduce-scatter -> Adam -> all-gather; bounded fits:
+        Adam on u, modes 2 / 3) as packed launch arguments for a compute launch that carries
+        it (fused exchange)."""
         a, b = self.own[c]
         o, n = self.loc_off[c], self.loc_len[c]
         tl = self._tl()
         traj = None if tl is None else tl.reshape(-1)[o:]
-        return self.twoshot.pack(a, b - a, 1, m=self.m[o:o + n], v=self.v[o:o + n], traj=traj,
+        bnd = self._bslice(c)
+        mode = 1 if bnd is None else (3 if self.legacy else 2)
+        return self.twoshot.pack(a, b - a, mode, m=self.m[o:o + n], v=self.v[o:o + n], traj=traj,
                                  traj_stride=0 if traj is None else self.traj_loc.shape[1],
                                  step=self.step_dev[c], host_step=self._hstep(), lr=self.lr,
-                                 b1=self.b1, b2=self.b2, eps=self.eps, max_blocks=self.ts_blocks)
+                                 b1=self.b1, b2=self.b2, eps=self.eps, max_blocks=self.ts_blocks,
+                                 u=None if self.u_loc is None else self.u_loc[o:o + n],
+                                 bounds=bnd)
 
     def _flush_exchange(self):
         """Launch the pending exchange of the last chunk on its own (fused exchange)."""

@@ -468,17 +468,21 @@ class TwoShot:
     def pack(self, lo: int, n: int, mode: int, m=None, v=None, traj=None, traj_stride: int = 0,
              step: Optional[torch.Tensor] = None, host_step: Optional[int] = None,
              lr: float = 0.0, b1: float = 0.9, b2: float = 0.999, eps: float = 1e-8,
-             max_blocks: int = 0) -> bytes:
-        """The launch arguments of one Adam exchange (unbounded: ``mode`` 1), packed for a
-        compute launch that runs it in its first workgroups (fused exchange,
-        csrc/twoshot.h; ops.smf ``exchange=``).  Nothing is enqueued here."""
+             max_blocks: int = 0, u=None, bounds=None) -> bytes:
+        """The launch arguments of one Adam exchange (``mode`` 1: unbounded; 2 / 3: bounded
+        with ``u`` and ``bounds`` of the owned slice), packed for a compute launch that runs
+        it in its first workgroups (fused exchange, csrc/twoshot.h; ops.smf ``exchange=``).
+        Nothing is enqueued here."""
         from ..ops._ext import ext
         if not self.regions:
             raise RuntimeError("two-shot context used after close() (its peer memory is "
                                "unmapped)")
+        lo_b = hi_b = kind = None
+        if bounds is not None:
+            lo_b, hi_b, kind = bounds.lo, bounds.hi, bounds.kind
         return ext().xgmi_twoshot_pack(
             self.gpeers, self.tpeers, self.fpeers, self.rank, int(lo), int(n), self.numel,
-            int(mode), None, m, v, None, None, None, traj,
+            int(mode), u, m, v, lo_b, hi_b, kind, traj,
             self._step0 if step is None else step, self.seq, self.err,
             [float(-1 if host_step is None else host_step), float(lr), float(b1), float(b2),
              float(eps), self.timeout_s, float(traj_stride), float(self._blocks(max_blocks))])

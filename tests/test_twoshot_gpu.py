@@ -126,7 +126,8 @@ def test_twoshot_adam_modes_match_reference():
         np.testing.assert_array_equal(out[0][0][mode][0], out[1][0][mode][0])
 
 
-def _engine_hashed(rank, size, twoshot, bounded, chunks, layout="auto", graph=None, side="auto"):
+def _engine_hashed(rank, size, twoshot, bounded, chunks, layout="auto", graph=None, side="auto",
+                   legacy=False):
     lane_order = "local" if layout == "lanes" else None
     if graph is not None:
         os.environ["MULTIGRAD_GRAPH"] = "1" if graph else "0"
@@ -148,7 +149,8 @@ def _engine_hashed(rank, size, twoshot, bounded, chunks, layout="auto", graph=No
         g = data["guess"].cpu()
         bounds = np.stack([g.numpy() - 0.5, g.numpy() + 0.7], 1)
         bounds[1::4, 1] = np.inf
-    traj = eng.run_adam(data["guess"], nsteps=5, learning_rate=1e-3, param_bounds=bounds)
+    traj = eng.run_adam(data["guess"], nsteps=5, learning_rate=1e-3, param_bounds=bounds,
+                        legacy_bounds_jacobian=legacy)
     sh = data["shard"]
     return (traj.cpu().numpy(), eng.twoshot is not None, eng.zero,
             f"{sh.layout}/{sh.lane_order}" if sh.layout == "lanes" else sh.layout,
@@ -425,28 +427,31 @@ def test_autotune_falls_back_to_rccl_when_no_peer_schedule_survives():
     assert np.isfinite(rec["loss_last"])
 
 
-def _engine_hashed_fused(rank, size, fused, chunks):
+def _engine_hashed_fused(rank, size, fused, chunks, bounded=False, legacy=False):
     os.environ["MULTIGRAD_TWOSHOT_FUSED"] = "on" if fused else "off"
     os.environ["MULTIGRAD_TWOSHOT_SIDE_STREAM"] = "off"
-    return _engine_hashed(rank, size, True, False, chunks, "auto", None, "off")
+    return _engine_hashed(rank, size, True, bounded, chunks, "auto", None, "off", legacy)
 
 
-@pytest.mark.parametrize("size,chunks", [(2, 2), (2, 3), (4, 2), (8, 4)])
-def test_engine_hashed_fused_exchange_matches_serial(size, chunks):
-    """the fused exchange -- chunk c-1's two-shot exchange in the first
-    workgroups of chunk c's VJP launch, the last chunk's in the next step's first forward
-    launch (no side stream, no events) -- gives the same bits as the serial two-shot
-    schedule (2, 4 and 8 processes on one GPU), and with 2 ranks as the RCCL/gloo path."""
-    ser = run_distributed(_engine_hashed_fused, size, False, chunks, timeout=900)
-    fus = run_distributed(_engine_hashed_fused, size, True, chunks, timeout=900)
+@pytest.mark.parametrize("size,chunks,bounded,legacy", [
+    (2, 2, False, False), (2, 3, False, False), (4, 2, False, False), (8, 4, False, False),
+    (2, 2, True, False), (4, 3, True, False), (2, 3, True, True)])
+def test_engine_hashed_fused_exchange_matches_serial(size, chunks, bounded, legacy):
+    """the fused exchange -- chunk c-1's two-shot exchange in the
+    first workgroups of chunk c's VJP launch, the last chunk's in the next step's first
+    forward launch (no side stream, no events) -- gives the same bits as the serial
+    two-shot schedule (2, 4 and 8 processes on one GPU), and with 2 ranks as the RCCL/gloo
+    path; unbounded (mode 1) and bounded (mode 2, mode 3 with the legacy Jacobian)."""
+    ser = run_distributed(_engine_hashed_fused, size, False, chunks, bounded, legacy, timeout=900)
+    fus = run_distributed(_engine_hashed_fused, size, True, chunks, bounded, legacy, timeout=900)
     assert all(r[1] and r[5] == chunks and "fused exchange" in r[4] for r in fus), fus[0][4]
     assert not any("fused exchange" in r[4] for r in ser)
     for r in range(size):
         np.testing.assert_array_equal(fus[r][0], fus[0][0])
         np.testing.assert_array_equal(fus[r][0], ser[r][0])
     if size == 2:
-        ref = run_distributed(_engine_hashed, 2, False, False, chunks, "auto", None, "off",
-                              timeout=600)
+        ref = run_distributed(_engine_hashed, 2, False, bounded, chunks, "auto", None, "off",
+                              legacy, timeout=600)
         np.testing.assert_array_equal(fus[0][0], ref[0][0])
 
 
