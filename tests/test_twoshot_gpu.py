@@ -129,6 +129,8 @@ def test_twoshot_adam_modes_match_reference():
 def _engine_hashed(rank, size, twoshot, bounded, chunks, layout="auto", graph=None, side="auto",
                    legacy=False):
     lane_order = "local" if layout == "lanes" else None
+    if layout == "lanes-global":  # global slot order: internal parameter order, residual VJP
+        layout, lane_order = "lanes", "global"
     if graph is not None:
         os.environ["MULTIGRAD_GRAPH"] = "1" if graph else "0"
     os.environ["MULTIGRAD_TWOSHOT_SIDE_STREAM"] = side
@@ -161,7 +163,8 @@ def _engine_hashed(rank, size, twoshot, bounded, chunks, layout="auto", graph=No
 @pytest.mark.parametrize("bounded,chunks,layout,side", [
     (False, 1, "auto", "auto"), (True, 1, "auto", "auto"), (False, 3, "auto", "on"),
     (True, 4, "auto", "on"), (False, 3, "auto", "off"), (True, 2, "auto", "auto"),
-    (False, 2, "lanes", "on")])
+    (False, 2, "lanes", "on"), (False, 2, "lanes-global", "auto"),
+    (True, 2, "lanes-global", "off")])
 def test_engine_hashed_twoshot_matches_rccl_path(bounded, chunks, layout, side):
     """One chunk, and several chunks whose exchanges run on the compute stream ("off"), on
     the side stream overlapping the next chunk's VJP and the next step's forward ("on"),
@@ -172,7 +175,7 @@ def test_engine_hashed_twoshot_matches_rccl_path(bounded, chunks, layout, side):
                           timeout=600)
     res = run_distributed(_engine_hashed, 2, True, bounded, chunks, layout, None, side,
                           timeout=600)
-    want = "tiles" if layout == "auto" else "lanes/local"
+    want = {"auto": "tiles", "lanes": "lanes/local", "lanes-global": "lanes/global"}[layout]
     assert all(r[2] and r[3] == want and r[5] == chunks for r in ref + res), ref[0][3]
     assert not ref[0][1] and res[0][1] and res[1][1], (ref[0][4], res[0][4])
     if chunks > 1:
