@@ -495,3 +495,35 @@ def test_load_state_dict_mid_run_discards_nothing_pending():
     same continuation as a fresh engine resumed from that checkpoint."""
     for ta, tb in run_distributed(_load_midrun, 2, timeout=600):
         np.testing.assert_array_equal(ta, tb)
+
+
+def _owner_relayout(rank, size, relayout):
+    os.environ["MULTIGRAD_RELAYOUT"] = "1" if relayout else "0"
+    os.environ["MULTIGRAD_RELAYOUT_EVERY"] = "4"
+    import multigrad_amd as mg
+    from multigrad_amd.engine.fused import FusedAdamEngine
+    from multigrad_amd.models.population import PopulationSMFModel, make_population_data
+    comm = mg.get_world_comm()
+    dev = torch.device("cuda", 0)
+    # 20% of the populations start wide and fit towards a narrow truth: they cross the
+    # Euler-Maclaurin limit during the run
+    data = make_population_data(6000, 300_000, seed=14, comm=comm, device=dev, placement="owner",
+                                narrow_frac=0.2, narrow_guess_log_sigma=-0.6)
+    model = PopulationSMFModel(aux_data=data, comm=comm)
+    model.set_target_from_truth()
+    eng = FusedAdamEngine(model, graph=False)
+    traj = eng.run_adam(data["guess"], nsteps=40, learning_rate=2e-2)
+    return traj.cpu().numpy(), eng.owner, [r["step"] for r in eng.relayouts]
+
+
+def test_owner_relayout_two_ranks_matches_static_layout():
+    """Re-layout under owner placement on 2 ranks: the ranks vote, re-lay out their own
+    shards at the same step, and the trajectory equals the run without re-layout."""
+    ref = run_distributed(_owner_relayout, 2, False, timeout=600)
+    res = run_distributed(_owner_relayout, 2, True, timeout=600)
+    assert all(r[1] for r in ref + res)
+    assert not ref[0][2] and res[0][2], (ref[0][2], res[0][2])
+    assert res[0][2] == res[1][2]  # the same steps on both ranks
+    for r in range(2):
+        np.testing.assert_allclose(res[r][0], ref[r][0], rtol=1e-5, atol=1e-6)
+    np.testing.assert_array_equal(res[0][0], res[1][0])
