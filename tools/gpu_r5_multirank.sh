@@ -10,7 +10,7 @@ for n in 4 8; do
   NPROC=$n PLACEMENT=hashed timeout -k 10 900 bash tools/bench_2rank.sh --steps 20 --warmup 5 --no-count-launches \
     > $O/bench_n$n.json 2> $O/bench_n$n.err || { tail -30 $O/bench_n$n.err; exit 1; }
   python -c "
-import json; d=json.load(open('$O/bench_n$n.json'))
+import json; d=json.loads([l for l in open('$O/bench_n$n.json') if l.startswith('{')][-1])  # gloo prints to stdout too
 print($n, d['value'], d['loss_last'], d['config']['grad_collective'])
 print(json.dumps(d['peer_memory_selftest'])[:600])
 print(json.dumps(d['config']['autotune'])[:800])"
