@@ -283,6 +283,13 @@ def main(argv=None):
     import multigrad_amd as mg
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    json_fd = None
+    if world > 1:
+        # every rank's fd 1 goes to stderr while it runs (gloo prints its connection
+        # messages to stdout), so rank 0's JSON record is the only line on stdout
+        sys.stdout.flush()
+        json_fd = os.dup(1)
+        os.dup2(2, 1)
     comm = mg.init_distributed() if world > 1 else mg.get_world_comm()
     if comm.size != args.gpus:
         raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started "
@@ -379,7 +386,11 @@ def main(argv=None):
         if own is not None and own is not head:
             rec["owner_phases_ms"] = own["phases_ms"]
     if comm.rank == 0:
-        print(json.dumps(rec), flush=True)
+        if json_fd is not None:
+            sys.stdout.flush()
+            os.write(json_fd, (json.dumps(rec) + "\n").encode())
+        else:
+            print(json.dumps(rec), flush=True)
     if comm.size > 1:
         comm.barrier()
         import torch.distributed as dist
