@@ -173,3 +173,30 @@ def test_launcher_env_fallbacks(monkeypatch):
     monkeypatch.setenv("OMPI_COMM_WORLD_LOCAL_RANK", "3")
     env = C.launcher_env()
     assert env["rank"] == 3 and env["size"] == 8 and env["local_rank"] == 3
+
+
+def _host_count_body(rank, size):
+    import multigrad_amd as mg
+    from multigrad_amd.optim._reduce import DeviceReducer
+    comm = mg.get_world_comm()
+    n0 = comm.host_collectives
+    t = torch.ones(3)
+    comm.all_reduce(t)
+    comm.barrier()
+    n1 = comm.host_collectives
+    # the optimizers' reducer on CPU tensors: the host path, one sum and one max all-reduce
+    red = DeviceReducer(comm, sharded=True, device="cpu")
+    out = red.reduce(sums=[torch.tensor([rank + 1.0, 2.0])], maxes=[torch.tensor([float(rank)])],
+                     local=[torch.tensor([7.0])])
+    return n1 - n0, comm.host_collectives - n1, red.describe(), out.tolist(), t.tolist()
+
+
+def test_host_collectives_are_counted_and_reducer_layout():
+    """TorchComm counts its host (gloo) collectives -- the device optimizers report the
+    count per run (0 on GPUs with peer memory or RCCL) -- and DeviceReducer returns
+    [sums, maxes, local] in one vector on every path."""
+    res = run_distributed(_host_count_body, 2)
+    for rank, (d_direct, d_red, path, out, t) in enumerate(res):
+        assert d_direct == 2 and d_red == 2 and path == "host"
+        assert out == [3.0, 4.0, 1.0, 7.0]
+        assert t == [2.0, 2.0, 2.0]
