@@ -15,12 +15,27 @@ def main():
     ap.add_argument("--so", required=True)
     ap.add_argument("--params", type=int, default=1_250_000)
     ap.add_argument("--halos", type=int, default=1 << 24)
+    ap.add_argument("--shuffle", action="store_true",
+                    help="hand the static LPT lists to the waves in a random order")
     a = ap.parse_args()
     import torch
     spec = importlib.util.spec_from_file_location("multigrad_amd._C", a.so)
     mod = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(mod)
     sys.modules["multigrad_amd._C"] = mod
+    if a.shuffle:
+        lpt = mod.lpt_waves
+
+        def shuffled(*args):
+            order, start = lpt(*args)
+            nw = start.numel() - 1
+            perm = torch.randperm(nw, generator=torch.Generator().manual_seed(7))
+            lens = (start[1:] - start[:-1])[perm]
+            lists = [order[start[w]:start[w + 1]] for w in perm.tolist()]
+            new_start = torch.zeros_like(start)
+            new_start[1:] = torch.cumsum(lens, 0)
+            return torch.cat(lists), new_start
+        mod.lpt_waves = shuffled
     from multigrad_amd.models.population import make_population_data
     from multigrad_amd.ops import smf as S
     dev = torch.device("cuda", 0)
