@@ -12,17 +12,21 @@ all-reduce of the sumstats, loss + cotangent, VJP over all halos, the cross-rank
 gradient sum, the Adam update of all 1e7 parameters, and the trajectory write of the new
 parameters.
 
-On N > 1 GPUs (one process per GPU) two placements of the same global catalog are timed
-back to back in one run:
+On N > 1 GPUs (one process per GPU) every rank starts from the reference's data
+parallelism: a contiguous block of halo indices (``np.array_split`` of the catalog,
+reference tests/smf_example/smf_grad_descent.py:28), so every rank touches every
+population.  Two schedules of that same input are timed back to back in one run:
 
-* ``value`` -- **hashed** placement, the reference's data parallelism (BASELINE config 3,
-  reference multigrad/multigrad.py:522,531-532): every rank holds a contiguous block of
-  halo indices, so every rank's gradient is dense over all 1e7 parameters and the engine
-  sums it across ranks every step (reduce-scatter -> Adam on the owned 1/N slice ->
-  all-gather, ZeRO-1; the same bytes as one all-reduce).
-* ``owner_steps_per_s`` -- **owner** placement: the catalog is split by population, each
-  rank's gradient is complete on the populations it owns, and the per-step collective is
-  the 10-float sumstat all-reduce only.
+* ``value`` -- the engine's default: at setup it **re-partitions** the halos by parameter
+  owner with one all-to-all-v (``Comm.all_to_all_v``: xGMI peer pulls, RCCL fallback;
+  ``models.population.repartition_by_owner``), after which each rank's gradient is
+  complete on the populations it owns and the only per-step collective is the 10-float
+  sumstat all-reduce.  ``setup_s`` includes the re-partition (``repartition`` in the
+  record has its own timing).
+* ``dense_steps_per_s`` -- the data-parallel schedule kept as it is (BASELINE config 3,
+  reference multigrad/multigrad.py:522,531-532): the dense 1e7-float gradient is summed
+  across ranks every step (reduce-scatter -> Adam on the owned 1/N slice -> all-gather,
+  ZeRO-1, the same bytes as one all-reduce) by the two-shot xGMI exchange or RCCL.
 
 Usage: ``python bench.py [--gpus N] [--steps K] [--warmup W]``.  With ``--gpus N > 1`` and no
 launcher environment the script starts ``torch.distributed.run`` with N ranks itself
@@ -52,11 +56,13 @@ def _args(argv=None):
                     help="global number of halos (fixed across GPU counts: strong scaling)")
     ap.add_argument("--lr", type=float, default=1e-3)
     ap.add_argument("--history", default="full", help="trajectory: full | last | <stride>")
-    ap.add_argument("--placement", default="both", choices=["both", "hashed", "owner"],
-                    help="halo -> rank placement timed for N > 1: 'hashed' (dense gradient "
-                         "summed across ranks every step: the headline value), 'owner' "
-                         "(catalog split by population), or 'both' (default: hashed is "
-                         "'value', owner is 'owner_steps_per_s')")
+    ap.add_argument("--placement", default="both",
+                    choices=["both", "repartition", "hashed", "owner"],
+                    help="schedule timed for N > 1: 'repartition' (hashed input re-partitioned "
+                         "by parameter owner at setup: the headline value), 'hashed' (dense "
+                         "gradient summed across ranks every step), 'owner' (catalog generated "
+                         "split by population), or 'both' (default: repartition is 'value', "
+                         "hashed is 'dense_steps_per_s')")
     ap.add_argument("--layout", default="auto", choices=["auto", "lanes", "tiles"],
                     help="device layout of the halo shards (auto: lanes for one rank and the "
                          "owner placement, tiles for hashed shards on several ranks)")
@@ -153,10 +159,13 @@ def time_placement(placement, args, comm, dev, sync):
     Returns the per-rank record (elapsed is the MAX over ranks)."""
     import torch
     from multigrad_amd.models.population import PopulationSMFModel, make_population_data
+    from multigrad_amd.utils.trace import trace
 
+    trace(f"bench: {placement}: data")
     t_setup = time.perf_counter()
+    gen = "owner" if placement == "owner" and comm.size > 1 else "hashed"
     data = make_population_data(args.params, args.halos, seed=1234, comm=comm, device=dev,
-                                placement=placement if comm.size > 1 else "hashed",
+                                placement=gen,
                                 layout=args.layout,
                                 lane_order=None if args.lane_order == "auto" else args.lane_order,
                                 narrow_frac=args.narrow_frac,
@@ -164,7 +173,8 @@ def time_placement(placement, args, comm, dev, sync):
     model = PopulationSMFModel(aux_data=data, comm=comm)
     model.set_target_from_truth()
     history = args.history if args.history in ("full", "last") else int(args.history)
-    engine = model.fused_engine(graph=False if (args.no_graph or args.profile_phases) else None)
+    engine = model.fused_engine(graph=False if (args.no_graph or args.profile_phases) else None,
+                                repartition=placement == "repartition")
     if args.profile_phases:  # HIP-event timing per phase (eager launches)
         from multigrad_amd.utils.profiling import PhaseTimer
         engine.timer = PhaseTimer(True)
@@ -174,6 +184,7 @@ def time_placement(placement, args, comm, dev, sync):
     sync()
     setup_s = time.perf_counter() - t_setup
 
+    trace(f"bench: {placement}: warmup")
     engine.steps(args.warmup)
     # the last warmup step's pending (pipelined) update is applied before the clock starts,
     # so the timed region holds exactly K forwards and K updates (the K-th one in drain())
@@ -182,6 +193,7 @@ def time_placement(placement, args, comm, dev, sync):
     sync()
     comm.barrier()
     sync()
+    trace(f"bench: {placement}: timed steps")
     t0 = time.perf_counter()
     phases = []
     if args.phase_steps > 0:
@@ -204,6 +216,7 @@ def time_placement(placement, args, comm, dev, sync):
     sync()
     comm.barrier()
     elapsed = time.perf_counter() - t0
+    trace(f"bench: {placement}: timed {elapsed:.4f} s")
     engine.check()  # a failed peer exchange raises here instead of reporting wrong numbers
     loss1 = engine.last_loss()
     fb = model.lane_fallback_groups(data["guess"])  # lane groups on the per-edge path
@@ -227,7 +240,9 @@ def time_placement(placement, args, comm, dev, sync):
         "pipelined": bool(engine.pipeline),
         "optimizer_sharding": ("owner" if engine.owner else "zero1" if engine.zero
                                else "replicated"),
-        "placement": data["placement"],
+        "placement": data["placement"] + (" (re-partitioned from hashed at setup)"
+                                          if engine.repartitioned else ""),
+        "repartition": engine.repartitioned or None,
         "grad_collective": engine.grad_collective_name(),
         "sumstat_allreduce": engine.sumstat_collective_name(),
         "chunks": engine.C,
@@ -308,7 +323,7 @@ def main(argv=None):
     if comm.size == 1:
         order = ["hashed"]  # one rank: the placements coincide
     elif args.placement == "both":
-        order = ["hashed", "owner"]
+        order = ["repartition", "hashed"]
     else:
         order = [args.placement]
     def release():
@@ -319,7 +334,7 @@ def main(argv=None):
     res, errors = run_placements(order, lambda p: time_placement(p, args, comm, dev, sync),
                                  on_error=release)
     head = res[order[0]]
-    own = res.get("owner", head if comm.size == 1 else None)
+    dense = res.get("hashed", head if comm.size == 1 else None)
     history = head["history"]
     rec = {
         "metric": "Adam steps/sec (whole node), 1e7-param summed-loss model",
@@ -361,12 +376,14 @@ def main(argv=None):
             "device_ops_per_step": head["device_ops_per_step"],
             "autotune": head["autotune"],
         },
-        "owner_steps_per_s": None if own is None else round(own["steps_per_s"], 3),
-        "owner_ms_per_step": None if own is None else round(own["ms_per_step"], 4),
+        "dense_steps_per_s": None if dense is None else round(dense["steps_per_s"], 3),
+        "dense_ms_per_step": None if dense is None else round(dense["ms_per_step"], 4),
         "loss_first_timed": head["loss_first_timed"],
         "loss_last": head["loss_last"],
         "setup_s": head["setup_s"],
     }
+    if head["repartition"]:
+        rec["repartition"] = head["repartition"]
     if head["phases"]:
         rec["phases"] = head["phases"]
     if comm.size > 1:
@@ -376,15 +393,16 @@ def main(argv=None):
         rec["peer_memory_selftest"] = status(comm)
     if errors:
         rec["errors"] = errors
-    if own is not None and own is not head:
-        rec["owner_config"] = {k: own[k] for k in ("parallelism", "optimizer_sharding",
-                                                   "grad_collective", "sumstat_allreduce",
-                                                   "chunks", "pipelined", "layout",
-                                                   "device_ops_per_step", "autotune", "graph")}
+    if dense is not None and dense is not head:
+        rec["dense_config"] = {k: dense[k] for k in ("parallelism", "optimizer_sharding",
+                                                     "grad_collective", "sumstat_allreduce",
+                                                     "chunks", "pipelined", "layout",
+                                                     "device_ops_per_step", "autotune", "graph",
+                                                     "loss_last", "setup_s")}
     if args.profile_phases:
         rec["phases_ms"] = head["phases_ms"]
-        if own is not None and own is not head:
-            rec["owner_phases_ms"] = own["phases_ms"]
+        if dense is not None and dense is not head:
+            rec["dense_phases_ms"] = dense["phases_ms"]
     if comm.rank == 0:
         if json_fd is not None:
             sys.stdout.flush()

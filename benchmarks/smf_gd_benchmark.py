@@ -45,6 +45,13 @@ def main(argv=None):
     t = time.perf_counter() - t0
     if comm.rank == 0:
         ips = args.num_steps / t
+        eng = getattr(model, "fused_step_engine", lambda: None)()
+        rec = dict(metric="Grad descent iterations/sec", value=ips, num_halos=args.num_halos,
+                   num_steps=args.num_steps, num_processes=comm.size,
+                   engine=None if eng is None else dict(schedule=eng.schedule,
+                                                        graph=eng.use_graph, stats=eng.stats),
+                   final_params=res.params[-1].tolist(), final_loss=float(res.loss[-1]))
+        print(json.dumps(rec), flush=True)
         print(f"Benchmark with {comm.size} processes {vars(args)}")
         print("=" * 70)
         print(f"Grad descent iterations/sec = {ips}")

@@ -62,6 +62,18 @@ void smf_epilogue(torch::Tensor slab, int64_t nrows, std::vector<double> edges,
                   torch::Tensor loss, torch::Tensor h, std::vector<int64_t> peers, int64_t rank,
                   c10::optional<torch::Tensor> seq, c10::optional<torch::Tensor> err,
                   double timeout_s, c10::optional<torch::Tensor> advance);
+int64_t smf2_max_bins();
+int64_t smf2_fwd_max_blocks(int64_t nb, bool log_sigma);
+void smf2_forward(torch::Tensor x, torch::Tensor theta, std::vector<double> edges,
+                  std::vector<double> scale, bool log_sigma, torch::Tensor slab, int64_t nblocks);
+void smf2_step(torch::Tensor slab, int64_t nrows, std::vector<double> edges, std::vector<double> scale,
+               bool log_sigma, std::vector<torch::Tensor> state, std::vector<double> scalars,
+               std::vector<int64_t> peers, int64_t rank, c10::optional<torch::Tensor> seq,
+               c10::optional<torch::Tensor> err, int64_t mode);
+void smf2_loop(torch::Tensor x, std::vector<double> edges, std::vector<double> scale, bool log_sigma,
+               std::vector<torch::Tensor> state, std::vector<double> scalars,
+               std::vector<int64_t> peers, int64_t rank, c10::optional<torch::Tensor> seq,
+               c10::optional<torch::Tensor> err, int64_t steps);
 // xgmi.hip
 int64_t xgmi_alloc(int64_t bytes);
 torch::Tensor xgmi_tensor(int64_t ptr, int64_t numel);
@@ -93,6 +105,8 @@ void xgmi_allreduce_wide(torch::Tensor x, int64_t nsum, int64_t nmax, std::vecto
                          int64_t rank, torch::Tensor seq, torch::Tensor err, double timeout_s);
 int64_t xgmi_wide_region_bytes();
 std::string device_pci_bus_id();
+void xgmi_a2a_pull(std::vector<int64_t> src_ptrs, std::vector<int64_t> counts,
+                   std::vector<int64_t> dst_offs, torch::Tensor out);
 // adam.hip
 void fused_adam(torch::Tensor u, torch::Tensor m, torch::Tensor v, torch::Tensor g,
                 c10::optional<torch::Tensor> p, c10::optional<torch::Tensor> lo,
@@ -171,6 +185,11 @@ PYBIND11_MODULE(_C, m) {
         pybind11::arg("S"), pybind11::arg("loss"), pybind11::arg("h"), pybind11::arg("peers"),
         pybind11::arg("rank"), pybind11::arg("seq"), pybind11::arg("err"), pybind11::arg("timeout_s"),
         pybind11::arg("advance") = pybind11::none());
+  m.def("smf2_max_bins", &mg::smf2_max_bins);
+  m.def("smf2_fwd_max_blocks", &mg::smf2_fwd_max_blocks);
+  m.def("smf2_forward", &mg::smf2_forward);
+  m.def("smf2_step", &mg::smf2_step);
+  m.def("smf2_loop", &mg::smf2_loop);
   m.def("xgmi_alloc", &mg::xgmi_alloc, pybind11::arg("bytes") = 0);
   m.def("xgmi_tensor", &mg::xgmi_tensor);
   m.def("xgmi_twoshot", &mg::xgmi_twoshot);
@@ -186,6 +205,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("xgmi_allreduce_wide", &mg::xgmi_allreduce_wide);
   m.def("xgmi_wide_region_bytes", &mg::xgmi_wide_region_bytes);
   m.def("device_pci_bus_id", &mg::device_pci_bus_id);
+  m.def("xgmi_a2a_pull", &mg::xgmi_a2a_pull);
   m.def("fused_adam", &mg::fused_adam, pybind11::arg("u"), pybind11::arg("m"), pybind11::arg("v"),
         pybind11::arg("g"), pybind11::arg("p"), pybind11::arg("lo"), pybind11::arg("hi"),
         pybind11::arg("kind"), pybind11::arg("step"), pybind11::arg("lr"), pybind11::arg("b1"),

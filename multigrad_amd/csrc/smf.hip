@@ -2851,4 +2851,626 @@ void smf_vjp_lanes_rc(torch::Tensor xi, torch::Tensor slot_idx, torch::Tensor sl
   }
 }
 
+// ======================================================= shared-parameter fused step (2 params)
+// The reference's own workload: the 2-parameter SMF models (tests/smf_example/
+// smf_grad_descent.py:32-82, docs/source/notebooks/smf_gradient_descent.py:19-91), every halo
+// sharing (a, s): mu_i = x_i + a, sigma = s (linear) or 10^s (LOGSIG).
+//
+// One shared sigma makes the bin width in sigma units h = delta / sigma ONE constant for
+// every halo, so the whole shard is a single "lane" of the Euler-Maclaurin forward above:
+// per halo, em_halo accumulates the Gaussian-factor sums F, Wa, E of the NB+1 edges from one
+// seed pair (3 v_exp + 1 v_rcp, no per-edge transcendental), and the lane constants (Q_j,
+// the trapezoid weight) are applied once per thread at the end.  Outside the EM range
+// (h > kEmHMax, or non-uniform / padded bins) the same loop evaluates the per-edge tails
+// (lane_halo_exact1).  Either way a thread ends with, per edge e, its cumulative mass C_e and
+// the VJP residuals G_e = sum f_e, W_e = sum f_e w_e -- and since both parameters are shared,
+// the gradient of the loss is LINEAR in those sums:
+//   dL/da = -(1/sigma) sum_e h_e G_e,   dL/ds = -(1/sigma or ln10) / kWScale sum_e h_e W_e
+// with the edge weights h_e of the cotangent (pop_grad).  So one pass over the halos gives
+// the sumstats AND everything the VJP needs: the 3 NB + 2 values (NB bin masses, NB+1 G,
+// NB+1 W) of every rank are summed across ranks in ONE 32-float one-shot exchange (NB = 10),
+// after which every rank forms the loss, the cotangent, the gradient and the optimizer
+// update of the two parameters in the same workgroup.  The reference needs a forward, an
+// all-reduce of the sumstats, a VJP over all halos and an all-reduce of the gradient
+// (multigrad/multigrad.py:508-538), with the second pass waiting on the first collective.
+//
+// Two schedules (engine/smf2.py): a grid forward + a one-workgroup step kernel per step
+// (large shards), or ONE persistent workgroup that runs many whole steps per launch (shards of
+// up to ~1e5 halos, where a step is a few microseconds and launches would dominate).
+template <int NB>
+struct S2 {
+  static constexpr int R = 3 * NB + 2;   // values per rank and step: masses, G, W
+};
+
+// halos per thread per round of the forward loop (loads of the next round in flight)
+#ifndef MG_S2_AHEAD
+#define MG_S2_AHEAD 2
+#endif
+constexpr int kS2Ahead = MG_S2_AHEAD;
+
+// Block sum of N values per thread, result in out[0..N) (LDS) for every thread after the
+// call: wave sums, then thread t < N adds the per-wave partials of value t -- N threads in
+// parallel instead of block_sum_n's serial loop over N * waves values on thread 0.
+template <int N, typename T>
+__device__ __forceinline__ void block_sum_par(T (&v)[N], T* scratch, T* out) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wid = threadIdx.x >> 6;
+  const int nw = blockDim.x >> 6;
+#pragma unroll
+  for (int k = 0; k < N; ++k) v[k] = wave_sum(v[k]);
+  if (lane == 0) {
+#pragma unroll
+    for (int k = 0; k < N; ++k) scratch[k * nw + wid] = v[k];
+  }
+  __syncthreads();
+  for (int k = threadIdx.x; k < N; k += blockDim.x) {
+    T s = scratch[k * nw];
+    for (int w = 1; w < nw; ++w) s += scratch[k * nw + w];
+    out[k] = s;
+  }
+  __syncthreads();
+}
+
+struct Smf2Step {
+  const float* target;
+  float* theta;       // [2] parameters p, read by the forwards
+  float* u;           // [2] optimizer coordinates (== p unless bounded)
+  float* m;
+  float* v;
+  int* step;          // [1] 0-based step index (device: graph / persistent-loop safe)
+  float* loss_hist;   // [nsteps] loss of step s
+  float* param_hist;  // [nsteps + 1][2]: row s = parameters at which loss s was evaluated
+  float* grad_out;    // [2] gradient of the last step
+  float* S_out;       // [NB] total sumstats of the last step
+  float* loss_out;    // [1]
+  float* vals;        // [R] split mode: the local sums out (mode 1) / the global sums in (mode 2)
+  float eps, lr, b1, b2, aeps;
+  float lo[2], hi[2];
+  int opt;            // 0 gradient descent, 1 Adam, 2 evaluate only (no update, no advance)
+  int legacy, bounded, nsteps, nb;
+  XgmiPeers peers;
+  int rank, size;
+  unsigned* seq;
+  int* err;
+  long long ticks;
+};
+
+template <int NB>
+__device__ __forceinline__ float pair_edge(const v2f (&P)[EdgePairs<NB>::NV], int e) {
+  using EP = EdgePairs<NB>;
+  const int i = e >> 1;
+  if (i < EP::NP) return (e & 1) ? P[i].y : P[i].x;
+  return P[i].x + P[i].y;
+}
+
+// This thread's share of one forward over halos [i0 + lane-strided, n): out[R] = bin masses,
+// G_e, W_e.  The loop is wave-uniform (masked lanes read the lane sentinel, which contributes
+// exactly zero on both paths), so the per-edge path's ballot counts are complete.
+template <int NB, bool LOGSIG>
+__device__ __forceinline__ void smf2_accumulate(const float* __restrict__ x, int64_t first,
+                                                int64_t n, int64_t stride, float a, float s,
+                                                const SmfBins& b, float (&out)[S2<NB>::R]) {
+  using EP = EdgePairs<NB>;
+  const float isig = inv_sigma<LOGSIG>(s);
+  const float inv = isig * kWScale;
+  const int lane = threadIdx.x & (kWave - 1);
+  v2f acc[EP::NV], G[EP::NV], W[EP::NV];
+  int cnt[NB + 1];
+#pragma unroll
+  for (int i = 0; i < EP::NV; ++i) acc[i] = G[i] = W[i] = (v2f)(0.0f);
+#pragma unroll
+  for (int e = 0; e <= NB; ++e) cnt[e] = 0;
+  // Software pipeline over the wave-strided halos: the kS2Ahead loads of the next round are
+  // in flight while this round is evaluated (a round's math alone does not cover the HBM
+  // latency at the occupancy these register footprints allow).
+  auto ld = [&](int64_t w0, float (&xs)[kS2Ahead]) {
+#pragma unroll
+    for (int u = 0; u < kS2Ahead; ++u) {
+      const int64_t i = w0 + (int64_t)u * stride + lane;
+      xs[u] = i < n ? x[i] : kLaneSentinel;
+    }
+  };
+  const int64_t step = (int64_t)kS2Ahead * stride;
+  // EM range: uniform unpadded bins and h = delta / sigma <= kEmHMax (a uniform branch)
+  if (b.delta > 0.0f && b.delta * isig <= kEmHMax) {
+    const EmLane L = em_lane(inv, b.delta);
+    const float nma = -a * inv;
+    v2f E[EP::NV];
+#pragma unroll
+    for (int i = 0; i < EP::NV; ++i) E[i] = (v2f)(0.0f);
+    float xa[kS2Ahead];
+    ld(first, xa);
+    for (int64_t w0 = first; w0 < n; w0 += step) {
+      float xb[kS2Ahead];
+      ld(w0 + step, xb);
+#pragma unroll
+      for (int u = 0; u < kS2Ahead; ++u) {
+        em_halo<NB, true>(fmaf(xa[u], -L.inv, nma), L.inv, L.dw4, L.a1, L.a3, L.a5, b, G, W, E);
+        xa[u] = xb[u];
+      }
+    }
+    em_group_end<NB>(L, G, W, E, acc);   // G, W become the residuals; acc the cumulative C_e
+  } else {
+    const float ninv = -inv, mua = a * inv;
+    float xa[kS2Ahead];
+    ld(first, xa);
+    for (int64_t w0 = first; w0 < n; w0 += step) {
+      float xb[kS2Ahead];
+      ld(w0 + step, xb);
+#pragma unroll
+      for (int u = 0; u < kS2Ahead; ++u) {
+        lane_halo_exact1<NB, true>(xa[u], ninv, mua, b, acc, cnt, G, W);
+        xa[u] = xb[u];
+      }
+    }
+  }
+  // the counts are per wave (every lane holds the same): folded in by lane 0 only
+  const bool counter = lane == 0;
+#pragma unroll
+  for (int k = 0; k < NB; ++k)
+    out[k] = (pair_edge<NB>(acc, k + 1) - pair_edge<NB>(acc, k)) +
+             (counter ? (float)(cnt[k + 1] - cnt[k]) : 0.0f);
+#pragma unroll
+  for (int e = 0; e <= NB; ++e) {
+    out[NB + e] = pair_edge<NB>(G, e);
+    out[2 * NB + 1 + e] = pair_edge<NB>(W, e);
+  }
+}
+
+// The step after the sums (whole block): cross-rank sum (one-shot, when size > 1 and peers
+// are mapped), loss + cotangent + edge weights, gradient from the residuals, the optimizer
+// update and the histories.  vals: R floats in LDS (the local sums in, clobbered).  thn: LDS
+// [2], the new parameters out (the persistent loop reads them).  Returns nothing; P.step is
+// advanced by thread 0 unless evaluating.
+template <int NB, bool LOGSIG>
+__device__ __forceinline__ void smf2_finish(const Smf2Step& P, const SmfBins& b, float* vals,
+                                            unsigned* seq, float* thn) {
+  constexpr int R = S2<NB>::R;
+  __shared__ float g[kMaxBins];
+  __shared__ float d2[kMaxBins];
+  if (P.size > 1) xgmi_block_allreduce(P.peers, P.rank, P.size, vals, R, seq, P.err, P.ticks);
+  const int k = threadIdx.x;
+  const int nb = P.nb;
+  if (k < nb) {
+    const float S = vals[k] * b.scale[k];
+    const float sv = S + P.eps;
+    const float d = log10f(sv) - log10f(P.target[k] + P.eps);
+    d2[k] = d * d;
+    g[k] = 2.0f / nb * d / (sv * kLn10);
+    if (P.opt != 2 || P.S_out) P.S_out[k] = S;
+  }
+  __syncthreads();
+  if (k == 0) {
+    float loss = 0.0f;
+    for (int j = 0; j < nb; ++j) loss += d2[j];
+    loss /= nb;
+    float A = 0.0f, B = 0.0f;
+#pragma unroll
+    for (int e = 0; e <= NB; ++e) {
+      const float h = e <= nb ? edge_weight(g, b, e, nb) : 0.0f;
+      A = fmaf(h, vals[NB + e], A);
+      B = fmaf(h, vals[2 * NB + 1 + e], B);
+    }
+    const float2 th = make_float2(P.theta[0], P.theta[1]);
+    const float2 gr = pop_grad<LOGSIG>(th, A, B);
+    P.loss_out[0] = loss;
+    P.grad_out[0] = gr.x;
+    P.grad_out[1] = gr.y;
+    float2 nt = th;
+    if (P.opt != 2) {
+      const int s = P.step[0];
+      if (s < P.nsteps) {
+        P.loss_hist[s] = loss;
+        P.param_hist[2 * s] = th.x;
+        P.param_hist[2 * s + 1] = th.y;
+      }
+      if (P.opt == 0) {  // reference multigrad/util.py:111: p <- p - lr g
+        nt.x = th.x - P.lr * gr.x;
+        nt.y = th.y - P.lr * gr.y;
+      } else {           // reference multigrad/adam.py:52-68 (csrc/adam.h, same bits)
+        const float bc1 = 1.0f - powf(P.b1, (float)(s + 1));
+        const float bc2 = 1.0f - powf(P.b2, (float)(s + 1));
+        struct { float lr, b1, b2, eps; } hp{P.lr, P.b1, P.b2, P.aeps};
+        const float gg[2] = {gr.x, gr.y};
+        const float po[2] = {th.x, th.y};
+        float pn[2];
+        for (int j = 0; j < 2; ++j) {
+          float uu = P.u[j], mm = P.m[j], vv = P.v[j];
+          if (P.bounded) {
+            const int8_t kd = bound_kind(P.lo[j], P.hi[j]);
+            if (P.legacy) adam_elem<true, true>(hp, bc1, bc2, gg[j], uu, mm, vv, po[j], P.lo[j], P.hi[j], kd, pn[j]);
+            else adam_elem<true, false>(hp, bc1, bc2, gg[j], uu, mm, vv, po[j], P.lo[j], P.hi[j], kd, pn[j]);
+          } else {
+            adam_elem<false, false>(hp, bc1, bc2, gg[j], uu, mm, vv, po[j], 0.0f, 0.0f, kNone, pn[j]);
+          }
+          P.u[j] = uu;
+          P.m[j] = mm;
+          P.v[j] = vv;
+        }
+        nt = make_float2(pn[0], pn[1]);
+      }
+      P.theta[0] = nt.x;
+      P.theta[1] = nt.y;
+      if (s + 1 <= P.nsteps) {
+        P.param_hist[2 * (s + 1)] = nt.x;
+        P.param_hist[2 * (s + 1) + 1] = nt.y;
+      }
+      P.step[0] = s + 1;
+    }
+    if (thn) {
+      thn[0] = nt.x;
+      thn[1] = nt.y;
+    }
+  }
+  __syncthreads();
+}
+
+template <int NB>
+struct S2Out {
+  float v[S2<NB>::R];
+};
+
+// The grid forward's per-edge path (h > kEmHMax or non-uniform bins), out of line so the hot
+// Euler-Maclaurin loop below is register-allocated on its own (as LMODE 3 of the lanes
+// kernel): the same wave-strided loop as the persistent kernel's.
+template <int NB, bool LOGSIG>
+__device__ __attribute__((noinline)) S2Out<NB> smf2_edge_pass(const float* __restrict__ x,
+                                                              int64_t first, int64_t n,
+                                                              int64_t stride, float a, float s,
+                                                              const SmfBins* bp) {
+  using EP = EdgePairs<NB>;
+  const SmfBins& b = *bp;
+  const float inv = inv_sigma<LOGSIG>(s) * kWScale;
+  const float ninv = -inv, mua = a * inv;
+  const int lane = threadIdx.x & (kWave - 1);
+  v2f acc[EP::NV], G[EP::NV], W[EP::NV];
+  int cnt[NB + 1];
+#pragma unroll
+  for (int i = 0; i < EP::NV; ++i) acc[i] = G[i] = W[i] = (v2f)(0.0f);
+#pragma unroll
+  for (int e = 0; e <= NB; ++e) cnt[e] = 0;
+  for (int64_t w0 = first; w0 < n; w0 += stride) {
+    const int64_t i = w0 + lane;
+    lane_halo_exact1<NB, true>(i < n ? x[i] : kLaneSentinel, ninv, mua, b, acc, cnt, G, W);
+  }
+  S2Out<NB> o;
+  const bool counter = lane == 0;
+#pragma unroll
+  for (int k = 0; k < NB; ++k)
+    o.v[k] = (pair_edge<NB>(acc, k + 1) - pair_edge<NB>(acc, k)) +
+             (counter ? (float)(cnt[k + 1] - cnt[k]) : 0.0f);
+#pragma unroll
+  for (int e = 0; e <= NB; ++e) {
+    o.v[NB + e] = pair_edge<NB>(G, e);
+    o.v[2 * NB + 1 + e] = pair_edge<NB>(W, e);
+  }
+  return o;
+}
+
+// Rows of 64 halos per LDS tile of the staged forward (two tiles per wave in flight).
+#ifndef MG_S2_ROWS
+#define MG_S2_ROWS 8
+#endif
+constexpr int kS2Rows = MG_S2_ROWS;
+
+template <int N>
+__device__ __forceinline__ void vmem_wait_n() {  // s_waitcnt vmcnt(N), expcnt / lgkmcnt untouched
+  static_assert(N >= 0 && N < 64, "vmcnt is 6 bits");
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | 0x0F70);
+  asm volatile("" ::: "memory");
+}
+
+// Euler-Maclaurin pass of the grid forward: every wave owns a contiguous range of 64-halo rows
+// and streams it through two LDS tiles with global_load_lds (no VGPRs for the loads in
+// flight: the next tile lands while this one is evaluated), one ds_read per halo.  The lanes
+// forward of the population model stages its groups the same way; a register-prefetch loop
+// measured 400 us per 1e8 halos (4 waves / SIMD at 102 VGPRs: the loads were not covered).
+template <int NB>
+__device__ __forceinline__ void smf2_em_staged(const float* __restrict__ x, int64_t n,
+                                               const EmLane& L, float nma, const SmfBins& b,
+                                               float* tiles, v2f (&G)[EdgePairs<NB>::NV],
+                                               v2f (&W)[EdgePairs<NB>::NV],
+                                               v2f (&E)[EdgePairs<NB>::NV]) {
+  constexpr int TH = kS2Rows * kWave;   // halos per tile
+  const int lane = threadIdx.x & (kWave - 1);
+  const int64_t nw = (int64_t)gridDim.x * (kThreads / kWave);
+  const int64_t gw = (int64_t)blockIdx.x * (kThreads / kWave) + (threadIdx.x >> 6);
+  const int64_t ntiles = (n + TH - 1) / TH;
+  const int64_t t0 = ntiles * gw / nw, t1 = ntiles * (gw + 1) / nw;
+  auto stage = [&](int64_t t, float* dst) {
+#pragma unroll
+    for (int r = 0; r < kS2Rows; ++r) {
+      int64_t i = t * TH + r * kWave + lane;
+      i = i < n ? i : n - 1;   // in bounds; masked at the use
+      __builtin_amdgcn_global_load_lds(x + i, dst + r * kWave, 4, 0, 0);
+    }
+  };
+  if (t0 < t1) stage(t0, tiles);
+  for (int64_t t = t0; t < t1; ++t) {
+    float* cur = tiles + ((t - t0) & 1) * TH;
+    if (t + 1 < t1) {
+      stage(t + 1, tiles + ((t - t0 + 1) & 1) * TH);
+      vmem_wait_n<kS2Rows>();   // this tile's rows landed, the next tile's may be in flight
+    } else {
+      vmem_wait_n<0>();
+    }
+#pragma unroll 1
+    for (int r = 0; r < kS2Rows; ++r) {
+      const int64_t i = t * TH + r * kWave + lane;
+      float xv = cur[r * kWave + lane];
+      xv = i < n ? xv : kLaneSentinel;
+      em_halo<NB, true>(fmaf(xv, -L.inv, nma), L.inv, L.dw4, L.a1, L.a3, L.a5, b, G, W, E);
+    }
+  }
+}
+
+// Grid forward of one step: slab row per workgroup (R floats).
+template <int NB, bool LOGSIG>
+__global__ __launch_bounds__(kThreads) void smf2_fwd_kernel(const float* __restrict__ x, int64_t n,
+                                                            const float* __restrict__ theta,
+                                                            SmfBins b, float* __restrict__ slab) {
+  using EP = EdgePairs<NB>;
+  constexpr int R = S2<NB>::R;
+  __shared__ float tiles[(kThreads / kWave) * 2 * kS2Rows * kWave];
+  const float a = theta[0], s = theta[1];
+  const int lane = threadIdx.x & (kWave - 1);
+  float v[R];
+  const float isig = inv_sigma<LOGSIG>(s);
+  if (b.delta > 0.0f && b.delta * isig <= kEmHMax) {
+    const float inv = isig * kWScale;
+    const EmLane L = em_lane(inv, b.delta);
+    v2f acc[EP::NV], G[EP::NV], W[EP::NV], E[EP::NV];
+#pragma unroll
+    for (int i = 0; i < EP::NV; ++i) acc[i] = G[i] = W[i] = E[i] = (v2f)(0.0f);
+    smf2_em_staged<NB>(x, n, L, -a * inv, b, tiles + (threadIdx.x >> 6) * 2 * kS2Rows * kWave,
+                       G, W, E);
+    em_group_end<NB>(L, G, W, E, acc);
+#pragma unroll
+    for (int k = 0; k < NB; ++k) v[k] = pair_edge<NB>(acc, k + 1) - pair_edge<NB>(acc, k);
+#pragma unroll
+    for (int e = 0; e <= NB; ++e) {
+      v[NB + e] = pair_edge<NB>(G, e);
+      v[2 * NB + 1 + e] = pair_edge<NB>(W, e);
+    }
+  } else {
+    const int64_t first = (int64_t)blockIdx.x * kThreads + (threadIdx.x - lane);
+    const S2Out<NB> o = smf2_edge_pass<NB, LOGSIG>(x, first, n, (int64_t)gridDim.x * kThreads,
+                                                   a, s, &b);
+#pragma unroll
+    for (int k = 0; k < R; ++k) v[k] = o.v[k];
+  }
+  __shared__ float scratch[R * (kThreads / kWave)];
+  __shared__ float sums[R];
+  block_sum_par<R>(v, scratch, sums);
+  for (int k = threadIdx.x; k < R; k += kThreads) slab[(int64_t)blockIdx.x * R + k] = sums[k];
+}
+
+// One workgroup: slab rows -> sums (fixed-order double) -> [exchange] -> loss, gradient,
+// update.  mode 0: the whole step; 1: sums only, to P.vals (the caller all-reduces them on
+// RCCL / gloo); 2: the step from the global sums in P.vals.
+template <int NB, bool LOGSIG>
+__global__ __launch_bounds__(kEpiThreads) void smf2_step_kernel(const float* __restrict__ slab,
+                                                                int nrows, Smf2Step P, SmfBins b,
+                                                                int mode) {
+  constexpr int R = S2<NB>::R;
+  __shared__ float vals[R];
+  __shared__ double scratch[R * (kEpiThreads / kWave)];
+  if (mode == 2) {
+    if (threadIdx.x < R) vals[threadIdx.x] = P.vals[threadIdx.x];
+    __syncthreads();
+  } else {
+    double v[R];
+#pragma unroll
+    for (int k = 0; k < R; ++k) v[k] = 0.0;
+    for (int r = threadIdx.x; r < nrows; r += kEpiThreads) {
+#pragma unroll
+      for (int k = 0; k < R; ++k) v[k] += (double)slab[(int64_t)r * R + k];
+    }
+    __shared__ double dsum[R];
+    block_sum_par<R>(v, scratch, dsum);
+    for (int k = threadIdx.x; k < R; k += kEpiThreads) vals[k] = (float)dsum[k];
+    __syncthreads();
+    if (mode == 1) {
+      if (threadIdx.x < R) P.vals[threadIdx.x] = vals[threadIdx.x];
+      return;
+    }
+  }
+  Smf2Step Q = P;
+  if (mode == 2) Q.size = 1;  // already summed across ranks
+  smf2_finish<NB, LOGSIG>(Q, b, vals, P.seq, nullptr);
+}
+
+// Persistent schedule: ONE workgroup of kS2LoopThreads runs `steps` whole optimizer steps
+// (forward over every local halo, block sums, exchange, loss, gradient, update) per launch.
+// The sequence number of the exchange is kept in LDS for the launch (one load, one store).
+constexpr int kS2LoopThreads = 512;   // 2 waves per SIMD: 256 VGPRs, no spills
+
+template <int NB, bool LOGSIG>
+__global__ __launch_bounds__(kS2LoopThreads) void smf2_loop_kernel(const float* __restrict__ x,
+                                                                   int64_t n, Smf2Step P,
+                                                                   SmfBins b, int steps) {
+  constexpr int R = S2<NB>::R;
+  __shared__ float vals[R];
+  __shared__ float th[2];
+  __shared__ unsigned seq_sh;
+  __shared__ float scratch[R * (kS2LoopThreads / kWave)];
+  if (threadIdx.x == 0) {
+    th[0] = P.theta[0];
+    th[1] = P.theta[1];
+    seq_sh = P.size > 1 ? *P.seq : 0u;
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & (kWave - 1);
+  const int64_t first = (int64_t)(threadIdx.x - lane);
+  for (int it = 0; it < steps; ++it) {
+    float v[R];
+    smf2_accumulate<NB, LOGSIG>(x, first, n, (int64_t)kS2LoopThreads, th[0], th[1], b, v);
+    block_sum_par<R>(v, scratch, vals);
+    smf2_finish<NB, LOGSIG>(P, b, vals, &seq_sh, th);
+  }
+  if (threadIdx.x == 0 && P.size > 1) *P.seq = seq_sh;
+}
+
+static Smf2Step make_s2(std::vector<torch::Tensor> t, std::vector<double> sc,
+                        const std::vector<int64_t>& peers, int64_t rank,
+                        c10::optional<torch::Tensor> seq, c10::optional<torch::Tensor> err,
+                        int nb, int R) {
+  // tensors: target, theta, u, m, v, step, loss_hist, param_hist, grad_out, S_out, loss_out, vals
+  TORCH_CHECK(t.size() == 12, "smf2: 12 state tensors expected");
+  // scalars: eps, lr, b1, b2, adam_eps, opt, legacy, bounded, nsteps, lo0, lo1, hi0, hi1, timeout_s
+  TORCH_CHECK(sc.size() == 14, "smf2: 14 scalars expected");
+  const char* names[12] = {"target", "theta", "u", "m", "v", "step", "loss_hist", "param_hist",
+                           "grad_out", "S_out", "loss_out", "vals"};
+  for (int i = 0; i < 12; ++i)
+    check_dev(t[i], names[i], i == 5 ? at::kInt : at::kFloat);
+  const int nsteps = (int)sc[8];
+  TORCH_CHECK(t[0].numel() >= nb && t[1].numel() >= 2 && t[2].numel() >= 2 && t[3].numel() >= 2 &&
+              t[4].numel() >= 2 && t[5].numel() >= 1 && t[6].numel() >= nsteps &&
+              t[7].numel() >= 2 * (nsteps + 1) && t[8].numel() >= 2 && t[9].numel() >= nb &&
+              t[10].numel() >= 1 && t[11].numel() >= R, "smf2: state tensor too small");
+  Smf2Step P{};
+  P.target = t[0].data_ptr<float>();
+  P.theta = t[1].data_ptr<float>();
+  P.u = t[2].data_ptr<float>();
+  P.m = t[3].data_ptr<float>();
+  P.v = t[4].data_ptr<float>();
+  P.step = t[5].data_ptr<int>();
+  P.loss_hist = t[6].data_ptr<float>();
+  P.param_hist = t[7].data_ptr<float>();
+  P.grad_out = t[8].data_ptr<float>();
+  P.S_out = t[9].data_ptr<float>();
+  P.loss_out = t[10].data_ptr<float>();
+  P.vals = t[11].data_ptr<float>();
+  P.eps = (float)sc[0];
+  P.lr = (float)sc[1];
+  P.b1 = (float)sc[2];
+  P.b2 = (float)sc[3];
+  P.aeps = (float)sc[4];
+  P.opt = (int)sc[5];
+  TORCH_CHECK(P.opt >= 0 && P.opt <= 2, "smf2: opt 0 (GD), 1 (Adam) or 2 (evaluate)");
+  P.legacy = (int)sc[6];
+  P.bounded = (int)sc[7];
+  P.nsteps = nsteps;
+  P.lo[0] = (float)sc[9];
+  P.lo[1] = (float)sc[10];
+  P.hi[0] = (float)sc[11];
+  P.hi[1] = (float)sc[12];
+  P.ticks = (long long)(sc[13] * 1e8);
+  P.nb = nb;
+  const int size = peers.empty() ? 1 : (int)peers.size();
+  TORCH_CHECK(size <= kXMaxRanks && rank >= 0 && rank < size, "smf2: bad rank/size");
+  TORCH_CHECK(R <= kXMaxFloats, "smf2: too many bins for the one-shot exchange");
+  for (int r = 0; r < kXMaxRanks; ++r)
+    P.peers.base[r] = r < (int)peers.size() ? reinterpret_cast<char*>(peers[r]) : nullptr;
+  P.rank = (int)rank;
+  P.size = size;
+  if (size > 1) {
+    TORCH_CHECK(seq.has_value() && err.has_value() && seq->defined() && err->defined(),
+                "smf2: a multi-rank exchange needs seq/err");
+    check_dev(*seq, "seq", at::kInt);
+    check_dev(*err, "err", at::kInt);
+    P.seq = reinterpret_cast<unsigned*>(seq->data_ptr<int>());
+    P.err = err->data_ptr<int>();
+  }
+  return P;
+}
+
+#define MG_DISPATCH_NB2(NBP, ...)                            \
+  switch (NBP) {                                             \
+    case 1: { constexpr int NB = 1; __VA_ARGS__; break; }    \
+    case 2: { constexpr int NB = 2; __VA_ARGS__; break; }    \
+    case 4: { constexpr int NB = 4; __VA_ARGS__; break; }    \
+    case 8: { constexpr int NB = 8; __VA_ARGS__; break; }    \
+    case 10: { constexpr int NB = 10; __VA_ARGS__; break; }  \
+    default: { constexpr int NB = 16; __VA_ARGS__; break; }  \
+  }
+
+int64_t smf2_max_bins() { return 16; }
+
+int64_t smf2_fwd_max_blocks(int64_t nb, bool log_sigma) {
+  const int nbp = padded_bins((int)nb);
+  TORCH_CHECK(nbp <= 16, "smf2: at most 16 (padded) bins");
+  int dev = 0;
+  hipGetDevice(&dev);
+  hipDeviceProp_t prop;
+  hipGetDeviceProperties(&prop, dev);
+  int occ = 0;
+  MG_DISPATCH_NB2(nbp, {
+    with_bool(log_sigma, [&](auto LS) {
+      (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(
+          &occ, (const void*)smf2_fwd_kernel<NB, decltype(LS)::value>, kThreads, 0);
+    });
+  });
+  return (int64_t)std::max(1, occ) * prop.multiProcessorCount;
+}
+
+// Grid forward (slab[nblocks][3 NB + 2]).
+void smf2_forward(torch::Tensor x, torch::Tensor theta, std::vector<double> edges,
+                  std::vector<double> scale, bool log_sigma, torch::Tensor slab, int64_t nblocks) {
+  check_dev(x, "x", at::kFloat);
+  check_dev(theta, "theta", at::kFloat);
+  check_dev(slab, "slab", at::kFloat);
+  const int nbp = padded_bins((int)scale.size());
+  TORCH_CHECK(nbp <= 16, "smf2: at most 16 (padded) bins");
+  TORCH_CHECK(theta.numel() >= 2, "smf2: theta needs 2 entries");
+  TORCH_CHECK(nblocks >= 1 && nblocks <= 65535, "smf2: bad block count");
+  const SmfBins b = make_bins(edges, scale, nbp);
+  auto stream = at::hip::getCurrentHIPStream();
+  MG_DISPATCH_NB2(nbp, {
+    TORCH_CHECK(slab.numel() >= nblocks * S2<NB>::R, "smf2: slab too small");
+    with_bool(log_sigma, [&](auto LS) {
+      hipLaunchKernelGGL((smf2_fwd_kernel<NB, decltype(LS)::value>), dim3(nblocks), dim3(kThreads), 0,
+                         stream, x.data_ptr<float>(), (int64_t)x.numel(), theta.data_ptr<float>(), b,
+                         slab.data_ptr<float>());
+    });
+  });
+}
+
+// The step kernel (mode 0 / 1 / 2, see smf2_step_kernel).
+void smf2_step(torch::Tensor slab, int64_t nrows, std::vector<double> edges, std::vector<double> scale,
+               bool log_sigma, std::vector<torch::Tensor> state, std::vector<double> scalars,
+               std::vector<int64_t> peers, int64_t rank, c10::optional<torch::Tensor> seq,
+               c10::optional<torch::Tensor> err, int64_t mode) {
+  check_dev(slab, "slab", at::kFloat);
+  const int nb = (int)scale.size();
+  const int nbp = padded_bins(nb);
+  TORCH_CHECK(nbp <= 16, "smf2: at most 16 (padded) bins");
+  TORCH_CHECK(mode >= 0 && mode <= 2, "smf2: mode 0, 1 or 2");
+  const SmfBins b = make_bins(edges, scale, nbp);
+  auto stream = at::hip::getCurrentHIPStream();
+  MG_DISPATCH_NB2(nbp, {
+    constexpr int R = S2<NB>::R;
+    TORCH_CHECK(mode == 2 || (nrows >= 1 && slab.numel() >= nrows * R), "smf2: slab too small");
+    Smf2Step P = make_s2(state, scalars, mode == 0 ? peers : std::vector<int64_t>(), rank, seq, err, nb, R);
+    with_bool(log_sigma, [&](auto LS) {
+      hipLaunchKernelGGL((smf2_step_kernel<NB, decltype(LS)::value>), dim3(1), dim3(kEpiThreads), 0,
+                         stream, slab.data_ptr<float>(), (int)nrows, P, b, (int)mode);
+    });
+  });
+}
+
+// Persistent loop: `steps` whole steps in one launch of one workgroup.
+void smf2_loop(torch::Tensor x, std::vector<double> edges, std::vector<double> scale, bool log_sigma,
+               std::vector<torch::Tensor> state, std::vector<double> scalars,
+               std::vector<int64_t> peers, int64_t rank, c10::optional<torch::Tensor> seq,
+               c10::optional<torch::Tensor> err, int64_t steps) {
+  check_dev(x, "x", at::kFloat);
+  const int nb = (int)scale.size();
+  const int nbp = padded_bins(nb);
+  TORCH_CHECK(nbp <= 16, "smf2: at most 16 (padded) bins");
+  TORCH_CHECK(steps >= 1 && steps <= (1 << 20), "smf2: 1..2^20 steps per launch");
+  const SmfBins b = make_bins(edges, scale, nbp);
+  auto stream = at::hip::getCurrentHIPStream();
+  MG_DISPATCH_NB2(nbp, {
+    constexpr int R = S2<NB>::R;
+    Smf2Step P = make_s2(state, scalars, peers, rank, seq, err, nb, R);
+    TORCH_CHECK((int64_t)P.nsteps >= 0, "smf2: bad nsteps");
+    with_bool(log_sigma, [&](auto LS) {
+      hipLaunchKernelGGL((smf2_loop_kernel<NB, decltype(LS)::value>), dim3(1), dim3(kS2LoopThreads), 0,
+                         stream, x.data_ptr<float>(), (int64_t)x.numel(), P, b, (int)steps);
+    });
+  });
+}
+
 }  // namespace mg

@@ -372,4 +372,75 @@ pybind11::bytes xgmi_twoshot_pack(std::vector<int64_t> gbufs, std::vector<int64_
 
 int64_t xgmi_twoshot_flag_bytes() { return kTsFlagBytes; }
 
+
+// ============================================================================ all-to-all-v
+// Pull-mode all-to-all-v over peer memory: the setup-time re-partition of a data-parallel
+// shard by parameter owner (parallel/alltoall.py, Comm.all_to_all_v).  Every rank has packed
+// its send rows by destination into an exported region; rank r reads source q's segment for
+// r (q's send displacement of r, C[q][r] 32-bit words) straight over the q<->r xGMI link and
+// writes it at r's receive displacement of q.  All W-1 incoming links are busy at once
+// (blockIdx.y walks the sources), where a ring would push every byte through one link per
+// hop.  Host barriers bracket the launch (every sender's packing is complete before it,
+// every pull after it), so no device flags are involved; the caller verifies per-segment
+// checksums before trusting the result.
+struct A2aSegs {
+  const uint32_t* src[kXMaxRanks];
+  int64_t n[kXMaxRanks];
+  int64_t dst[kXMaxRanks];
+};
+
+constexpr int kA2aThreads = 256;
+constexpr int kA2aUnroll = 4;
+
+__global__ __launch_bounds__(kA2aThreads) void xgmi_a2a_pull_kernel(A2aSegs s,
+                                                                    uint32_t* __restrict__ out) {
+  const int q = blockIdx.y;
+  const uint32_t* __restrict__ src = s.src[q];
+  uint32_t* __restrict__ dst = out + s.dst[q];
+  const int64_t n = s.n[q];
+  const int64_t S = (int64_t)gridDim.x * kA2aThreads;
+  int64_t i = (int64_t)blockIdx.x * kA2aThreads + threadIdx.x;
+  // kA2aUnroll independent remote loads in flight per thread before the stores
+  for (; i + (kA2aUnroll - 1) * S < n; i += kA2aUnroll * S) {
+    uint32_t v[kA2aUnroll];
+#pragma unroll
+    for (int k = 0; k < kA2aUnroll; ++k) v[k] = src[i + k * S];
+#pragma unroll
+    for (int k = 0; k < kA2aUnroll; ++k) dst[i + k * S] = v[k];
+  }
+  for (; i < n; i += S) dst[i] = src[i];
+}
+
+// out[dst_offs[q] : + counts[q]] = words at src_ptrs[q] (peer addresses, already offset to the
+// segment), for every source q; counts / offsets in 32-bit words.  Launched on the current
+// stream; the caller synchronises.
+void xgmi_a2a_pull(std::vector<int64_t> src_ptrs, std::vector<int64_t> counts,
+                   std::vector<int64_t> dst_offs, torch::Tensor out) {
+  const int nsrc = (int)src_ptrs.size();
+  TORCH_CHECK(nsrc >= 1 && nsrc <= kXMaxRanks && (int)counts.size() == nsrc &&
+              (int)dst_offs.size() == nsrc, "all-to-all pull: 1..8 sources, one count/offset each");
+  TORCH_CHECK(out.is_cuda() && out.is_contiguous() && out.element_size() == 4,
+              "all-to-all pull: contiguous 32-bit device output");
+  A2aSegs s;
+  int64_t nmax = 0;
+  for (int q = 0; q < kXMaxRanks; ++q) {
+    s.src[q] = q < nsrc ? reinterpret_cast<const uint32_t*>(src_ptrs[q]) : nullptr;
+    s.n[q] = q < nsrc ? counts[q] : 0;
+    s.dst[q] = q < nsrc ? dst_offs[q] : 0;
+    if (q < nsrc) {
+      TORCH_CHECK(counts[q] >= 0 && dst_offs[q] >= 0 && dst_offs[q] + counts[q] <= out.numel(),
+                  "all-to-all pull: segment ", q, " outside the output");
+      TORCH_CHECK(counts[q] == 0 || (src_ptrs[q] != 0 && (src_ptrs[q] & 3) == 0),
+                  "all-to-all pull: segment ", q, " has no 4-byte aligned source");
+      nmax = std::max(nmax, counts[q]);
+    }
+  }
+  if (nmax == 0) return;
+  const int64_t per = (int64_t)kA2aThreads * kA2aUnroll;
+  const int gx = (int)std::max<int64_t>(1, std::min<int64_t>((nmax + per - 1) / per, 2048));
+  hipLaunchKernelGGL(xgmi_a2a_pull_kernel, dim3(gx, nsrc), dim3(kA2aThreads), 0,
+                     at::hip::getCurrentHIPStream(), s,
+                     reinterpret_cast<uint32_t*>(out.data_ptr()));
+}
+
 }  // namespace mg

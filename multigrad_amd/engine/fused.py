@@ -66,6 +66,7 @@ from ..optim.adam import History
 from ..optim.transforms import Bounds, KIND_NONE
 from ..ops.adam import adam_step_
 from ..utils.profiling import PhaseTimer
+from ..utils.trace import trace
 
 __all__ = ["FusedAdamEngine", "plan_chunks"]
 
@@ -147,7 +148,7 @@ class FusedAdamEngine:
 
     def __init__(self, model, comm=None, graph: Optional[bool] = None,
                  zero: Optional[bool] = None, chunks: Optional[int] = None,
-                 owner: Optional[bool] = None):
+                 owner: Optional[bool] = None, repartition: Optional[bool] = None):
         self.model = model
         self.comm = model.comm if comm is None else comm
         self.size = 1 if self.comm is None else self.comm.size
@@ -160,6 +161,15 @@ class FusedAdamEngine:
         self.allow_owner = True if o is None else bool(o)
         self.force_owner = bool(o)
         self.owner = False
+        # re-partition a data-parallel (hashed) shard by parameter owner at setup: one
+        # all-to-all-v of the data (model.engine_repartition), after which owner mode needs
+        # only the sumstat all-reduce per step.  None = on for several ranks unless owner
+        # mode or ZeRO was asked for explicitly; MULTIGRAD_REPARTITION overrides
+        r = _env_flag("MULTIGRAD_REPARTITION", repartition)
+        if r is None:
+            r = self.size > 1 and self.allow_owner and z is None
+        self.repartition = bool(r) and self.size > 1 and self.allow_owner
+        self.repartitioned = None  # the model's re-partition record, once done
         self.fuse_vjp_adam = bool(_env_flag("MULTIGRAD_FUSED_VJP_ADAM", True))
         # slab reduction (+ one-shot cross-rank sum) + loss in one launch
         self.fuse_epilogue = bool(_env_flag("MULTIGRAD_FUSED_EPILOGUE", True))
@@ -235,6 +245,7 @@ class FusedAdamEngine:
         kw = dict(param_bounds=param_bounds, learning_rate=learning_rate, b1=b1, b2=b2,
                   eps=eps, history=history, legacy_bounds_jacobian=legacy_bounds_jacobian)
         self._chunks_override = None
+        self._maybe_repartition()
         self._setup(guess, nsteps, **kw)
         tun = self.tuning
         if not (tun and self.twoshot is not None and not self.owner and self.C == 2
@@ -327,11 +338,14 @@ class FusedAdamEngine:
         hint = getattr(md, "engine_layout_hint", None)
         if hint is not None:  # e.g. lanes grouped by forward path at the starting point
             hint(guess)
+        trace(f"engine: layout ({'owner' if self.owner else 'dense'}, {len(ub) - 1} chunks)")
         md.engine_set_chunks(ub)
         self._ub = list(ub)
         if self.size > 1 and dev.type == "cuda" and self.fuse_epilogue:
             from ..parallel.xgmi import get_oneshot
+            trace("engine: one-shot connect")
             self.oneshot = get_oneshot(self.comm)  # collective (all ranks run setup)
+            trace(f"engine: one-shot {'up' if self.oneshot is not None else 'unavailable'}")
         # Internal order: models may keep the engine vectors in their own unit order
         # (e.g. the lanes layout's slot order, for coalesced parameter/gradient access).
         # It must keep every chunk's units inside the chunk, and be the same on all ranks;
@@ -712,7 +726,14 @@ class FusedAdamEngine:
             return None
         return self.history.buf.reshape(-1)
 
-    def _autotune(self, cands, warm: int = 2, min_window_s: float = 0.008,
+    def _autotune(self, cands, warm: int = 2, min_window_s: float = 0.008, **kw):
+        trace(f"engine: autotune {cands}")
+        try:
+            return self._autotune_impl(cands, warm, min_window_s, **kw)
+        finally:
+            trace(f"engine: autotune done {getattr(self, 'tuning', None)}")
+
+    def _autotune_impl(self, cands, warm: int = 2, min_window_s: float = 0.008,
                   max_reps: int = 400):
         """Collective: time each candidate schedule (a dict of engine attributes) over a
         window of at least ``min_window_s`` of work after ``warm`` steps, with syncs only
@@ -999,6 +1020,20 @@ class FusedAdamEngine:
             return False  # once per matching candidate
         seen.add(ck)
         return True
+
+    def _maybe_repartition(self) -> None:
+        """Collective: move the model's data to the parameter owners once (see
+        ``repartition`` in ``__init__``); a model without ``engine_repartition``, or whose
+        data already follow the owners, is left as it is."""
+        if not self.repartition or self.repartitioned is not None:
+            return
+        fn = getattr(self.model, "engine_repartition", None)
+        if fn is None:
+            return
+        trace("engine: re-partition by owner")
+        info = fn()
+        self.repartitioned = dict(info) if info else {}
+        trace(f"engine: re-partition done {self.repartitioned}")
 
     def _owner_units(self, md, J):
         """Owner-mode unit bounds if the model's data placement allows it on every rank."""

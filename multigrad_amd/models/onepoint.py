@@ -65,6 +65,15 @@ class _OptimizerFrontEnds:
                 and (loss_aux_ok or not any(m.loss_func_has_aux for m in members))
                 and os.environ.get("MULTIGRAD_GENERIC_ENGINE", "1") != "0")
 
+    def _step_engine(self, x0, comm=None):
+        """The model's cached fused step engine (``fused_step_engine``: the shared-parameter
+        SMF models, engine/smf2.py) for an fp32 device guess, or None."""
+        fn = getattr(self, "fused_step_engine", None)
+        if fn is None or not (x0.is_cuda and x0.dtype == torch.float32) or \
+                os.environ.get("MULTIGRAD_GENERIC_ENGINE", "1") == "0":
+            return None
+        return fn(comm=self._opt_comm() if comm is None else comm)
+
     def run_simple_grad_descent(self, guess, nsteps: int = 100, learning_rate: float = 0.01):
         """Fixed-learning-rate gradient descent.
 
@@ -73,6 +82,10 @@ class _OptimizerFrontEnds:
         """
         has_aux = bool(getattr(self, "loss_func_has_aux", False))
         x0 = as_param_tensor(guess, device=self.param_device())
+        eng = self._step_engine(x0)
+        if eng is not None and not has_aux:
+            # fused device step (engine/smf2.py): one pass + one exchange per step
+            return eng.run_simple_grad_descent(x0, nsteps=nsteps, learning_rate=learning_rate)
         if self._generic_engine_ok(x0, loss_aux_ok=False):
             # one captured step replayed per iteration (engine/generic.py)
             from ..engine.generic import GraphAdamEngine
@@ -109,6 +122,13 @@ class _OptimizerFrontEnds:
         fused = getattr(self, "fused_engine", None)
         use_engine = kw.pop("use_engine", True)
         keyed = randkey is not None or const_randkey
+        step_kw = ("history", "legacy_bounds_jacobian", "b1", "b2", "eps", "callback")
+        if use_engine and all(k in step_kw for k in kw) and (
+                not keyed or getattr(self, "engine_randkey_invariant", False)):
+            eng = self._step_engine(guess, comm)
+            if eng is not None:
+                return eng.run_adam(guess, nsteps=nsteps, param_bounds=param_bounds,
+                                    learning_rate=learning_rate, **kw)
         if fused is not None and use_engine and (
                 not keyed or getattr(self, "engine_randkey_invariant", False)):
             # a fused-protocol model whose hooks ignore randkey gives the same trajectory
@@ -154,7 +174,12 @@ class _OptimizerFrontEnds:
         if method == "scipy":
             fn = self.calc_loss_and_grad_from_params
             eng = None
-            if self._generic_engine_ok(x0):
+            step_eng = self._step_engine(x0, comm) if (
+                getattr(self, "engine_randkey_invariant", False) or randkey is None) else None
+            if step_eng is not None:
+                # each scipy evaluation is one fused device evaluation (engine/smf2.py)
+                fn = step_eng.evaluator()
+            elif self._generic_engine_ok(x0):
                 # each scipy evaluation replays one captured evaluation (engine/generic.py)
                 from ..engine.generic import GraphAdamEngine
                 eng = GraphAdamEngine(self, comm=comm)

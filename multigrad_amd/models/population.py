@@ -31,7 +31,8 @@ from ..ops.smf import (PopulationShard, SmfBins, logmse_loss, prepare_forward, s
 from ..parallel.comm import get_world_comm
 from .onepoint import OnePointModel
 
-__all__ = ["PopulationSMFModel", "make_population_data", "hash_uniform", "owner_bounds"]
+__all__ = ["PopulationSMFModel", "make_population_data", "hash_uniform", "owner_bounds",
+           "owner_bounds_from_counts", "repartition_by_owner"]
 
 _M1 = -7046029254386353131   # 0x9E3779B97F4A7C15 as int64
 _M2 = -4658895280553007687   # 0xBF58476D1CE4E5B9
@@ -75,15 +76,87 @@ def owner_bounds(num_halos: int, npop: int, seed: int, size: int, device) -> lis
     for a in range(0, int(num_halos), _GEN_CHUNK):
         idx = torch.arange(a, min(int(num_halos), a + _GEN_CHUNK), dtype=torch.int64, device=device)
         counts += torch.bincount(_global_pop(idx, seed, npop), minlength=npop)
-    cum = torch.cumsum(counts, 0).cpu().numpy()
+    return owner_bounds_from_counts(counts, size)
+
+
+def owner_bounds_from_counts(counts: torch.Tensor, size: int) -> list:
+    """:func:`owner_bounds` from the global per-population halo counts ``[J]`` (any device):
+    ``size`` contiguous, even-aligned population ranges of nearly equal halo counts."""
+    npop = int(counts.numel())
+    cum = torch.cumsum(counts.to(torch.int64), 0).cpu().numpy()
+    total = int(cum[-1]) if npop else 0
     bounds = [0]
     for r in range(1, size):
-        target = r * int(num_halos) / size
+        target = r * total / size
         q = int(np.searchsorted(cum, target, side="left")) + 1   # first pop after the split
         q = min(max(q - (q & 1), bounds[-1]), npop)
         bounds.append(q)
     bounds.append(npop)
     return bounds
+
+
+def repartition_by_owner(data: dict, comm=None, layout: str = "lanes",
+                         lane_order: str = "global") -> dict:
+    """Re-partition a data-parallel population shard by parameter owner, in place.
+
+    ``data`` is any rank's shard of the population model (:func:`make_population_data`
+    with ``placement="hashed"``, or a user's ``np.array_split`` of a catalog -- reference
+    tests/smf_example/smf_grad_descent.py:28).  Collective over ``comm``:
+
+    1. the per-population halo counts are summed across ranks (one all-reduce of ``J``
+       int64) and cut into ``W`` contiguous population ranges of nearly equal halo counts
+       (:func:`owner_bounds_from_counts`, the rule of the ``"owner"`` placement);
+    2. the shard is already sorted by population, so the halos bound for rank ``d`` are one
+       contiguous run: ONE all-to-all-v of ``(log mass, population)`` rows
+       (:meth:`Comm.all_to_all_v`: xGMI peer pulls, RCCL or gloo) moves every halo to the
+       rank that owns its population;
+    3. the received rows (source ranks in order, each sorted by population and, within a
+       population, in the source's order) are rebuilt into a shard in ``layout``.
+
+    A halo's order inside its population is its order in the concatenation of the source
+    shards, so an ``array_split`` of a catalog gives exactly the shard the ``"owner"``
+    placement generates.  Afterwards every rank's gradient is complete on its own
+    populations and zero elsewhere: the fused engine's owner mode drops the P-float gradient
+    all-reduce (reference multigrad/multigrad.py:531-532) and keeps only the sumstat
+    all-reduce.  Returns ``data`` (``shard``, ``placement="owner"``, ``owner_units`` and
+    ``repartition`` -- timing and row counts -- replaced)."""
+    import time
+    comm = get_world_comm() if comm is None else comm
+    t0 = time.perf_counter()
+    sh: PopulationShard = data["shard"]
+    if sh.pop is None:
+        raise ValueError("repartition_by_owner needs a population shard (pop ids)")
+    dev = sh.device
+    npop = sh.npop
+    gcounts = sh.counts.to(dev, torch.int64)
+    if comm.size > 1:
+        comm.all_reduce(gcounts)
+    bounds = owner_bounds_from_counts(gcounts, comm.size)
+    off = sh.offsets                                   # local cumsum of counts (host)
+    send_counts = [int(off[bounds[d + 1]] - off[bounds[d]]) for d in range(comm.size)]
+    rows = torch.stack([sh.x.reshape(-1).view(torch.int32), sh.pop.reshape(-1).to(torch.int32)], 1)
+    n_before = int(rows.shape[0])
+    from ..utils.trace import trace
+    trace(f"repartition: owner bounds done, all-to-all-v of {n_before} rows")
+    recv, recv_counts = comm.all_to_all_v(rows, send_counts)
+    trace("repartition: all-to-all-v done, building the owner shard")
+    del rows
+    t_x = time.perf_counter() - t0
+    x = recv[:, 0].contiguous().view(torch.float32)
+    pop = recv[:, 1].contiguous()
+    del recv
+    chunks = 1
+    new = PopulationShard(x, pop, npop, device=dev, chunks=chunks, layout=layout, comm=comm,
+                          lane_order=lane_order)
+    del x, pop
+    data["shard"] = new
+    data["placement"] = "owner"
+    data["owner_units"] = bounds
+    data["repartition"] = {"halos_before": n_before, "halos_after": int(new.n),
+                           "sent_to": send_counts, "received_from": list(recv_counts),
+                           "exchange_s": round(t_x, 4),
+                           "total_s": round(time.perf_counter() - t0, 4)}
+    return data
 
 
 def make_population_data(num_params: int = 10_000_000, num_halos: int = 1 << 27, seed: int = 0,
@@ -311,6 +384,18 @@ class PopulationSMFModel(OnePointModel):
     def engine_layout_share(self, chunk=None) -> float:
         """The per-edge group share the current lane classes imply (host)."""
         return self.shard.per_edge_share(chunk)
+
+    def engine_repartition(self) -> Optional[dict]:
+        """Fused-engine hook (collective): a data-parallel shard on several ranks is moved
+        to the parameter owners (:func:`repartition_by_owner`: one all-to-all-v), so the
+        engine runs in owner mode.  Returns the re-partition record, or None when there is
+        nothing to do (one rank, data already placed by owner)."""
+        d = self.aux_data
+        if self.comm is None or self.comm.size == 1 or d.get("placement") == "owner" \
+                or self.shard.pop is None:
+            return None
+        repartition_by_owner(d, self.comm)
+        return d["repartition"]
 
     def engine_owner_units(self):
         """Population (unit) bounds ``[W+1]`` of the owner placement, or None."""

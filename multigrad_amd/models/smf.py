@@ -84,10 +84,22 @@ class _SmfBase(OnePointModel):
 
     _log_sigma = False
     _loss_eps = 0.0
+    # the hooks ignore randkey (deterministic), so keyed runs may take the fused step
+    engine_randkey_invariant = True
+
+    def fused_step_engine(self, comm=None):
+        """The cached fused GD / Adam / evaluation engine of this model on the GPU
+        (:class:`multigrad_amd.engine.smf2.Smf2Engine`: one pass over the halos and one
+        32-float exchange per step), or None (CPU, relative tails, > 16 bins)."""
+        from ..engine.smf2 import Smf2Engine
+        return Smf2Engine.for_model(self, comm)
 
     def _setup(self):
         dev = self.param_device()
-        key = (str(dev),)
+        # rebuilt when the device or any aux_data entry is replaced (the cached fused step
+        # engine follows the shard it was built on, engine/smf2.py)
+        ad = self.aux_data or {}
+        key = (str(dev), id(ad)) + tuple((k, id(ad[k])) for k in sorted(ad))
         if getattr(self, "_cache_key", None) != key:
             lhm = torch.as_tensor(np.asarray(self.aux_data["log_halo_masses"]), dtype=torch.float32)
             self._shard = PopulationShard(lhm, None, 1, device=dev)

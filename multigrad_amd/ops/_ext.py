@@ -21,6 +21,16 @@ def ext():
         return _EXT
     try:
         import torch  # noqa: F401  (loads libamdhip64/libtorch before _C)
+        so = os.environ.get("MULTIGRAD_EXT_SO")
+        if so:  # an A/B build variant (tools/build_variant.sh) in place of the in-tree _C.so
+            import sys
+            from importlib import util as ilu
+            spec = ilu.spec_from_file_location("multigrad_amd._C", so)
+            mod = ilu.module_from_spec(spec)
+            spec.loader.exec_module(mod)
+            sys.modules["multigrad_amd._C"] = mod
+            _EXT = mod
+            return _EXT
         _EXT = importlib.import_module("multigrad_amd._C")
         return _EXT
     except ImportError as e:  # pragma: no cover - depends on build state

@@ -209,6 +209,19 @@ class Comm:
     def split(self, color, key: int = 0) -> Optional["Comm"]:
         raise NotImplementedError
 
+    def all_to_all_v(self, tensor: torch.Tensor, send_counts, counts=None):
+        """Collective all-to-all-v of rows: ``send_counts[d]`` consecutive rows of ``tensor``
+        go to rank ``d``; returns ``(rows received, in source-rank order; recv_counts)``.
+        Device tensors move over peer memory (xGMI pulls) or RCCL, host tensors over gloo
+        (parallel/alltoall.py).  ``counts``: the ``[src][dst]`` row-count matrix if known."""
+        from .alltoall import all_to_all_v
+        return all_to_all_v(self, tensor, send_counts, counts)
+
+    def _all_to_all_base(self, out: torch.Tensor, tensor: torch.Tensor, recv_counts,
+                         send_counts) -> str:
+        """Backend all-to-all-v into a preallocated ``out``; returns the path's name."""
+        raise NotImplementedError
+
 
 class _DoneWork:
     """Completed work handle (for async_op on trivially-complete collectives)."""
@@ -266,6 +279,10 @@ class SerialComm(Comm):
     def reduce_scatter_tensor(self, output, tensor, op=SUM, async_op=False):
         output.reshape(-1).copy_(tensor.reshape(-1))
         return _DoneWork() if async_op else None
+
+    def _all_to_all_base(self, out, tensor, recv_counts, send_counts):
+        out.copy_(tensor)
+        return "local copy"
 
     def split(self, color, key=0):
         if color is None or (isinstance(color, int) and color < 0):
@@ -422,6 +439,23 @@ class TorchComm(Comm):
         n = output.numel()
         output.reshape(-1).copy_(tmp[self.rank * n:(self.rank + 1) * n].to(output.device))
         return _DoneWork() if async_op else None
+
+    def _all_to_all_base(self, out, tensor, recv_counts, send_counts):
+        c10d = _c10d()
+        backend, staged = self._backend_for(tensor)
+        rc, sc = [int(c) for c in recv_counts], [int(c) for c in send_counts]
+        if backend is self._dev:
+            backend.alltoall_base(out, tensor, rc, sc, c10d.AllToAllOptions()).wait()
+            return "rccl alltoall"
+        self.host_collectives += 1
+        if staged:
+            host_out = torch.empty(out.shape, dtype=out.dtype)
+            self._cpu.alltoall_base(host_out, tensor.detach().cpu(), rc, sc,
+                                    c10d.AllToAllOptions()).wait()
+            out.copy_(host_out)
+            return "gloo alltoall (staged through host)"
+        self._cpu.alltoall_base(out, tensor, rc, sc, c10d.AllToAllOptions()).wait()
+        return "gloo alltoall"
 
     # ------------------------------------------------------------------ objects
     def barrier(self) -> None:

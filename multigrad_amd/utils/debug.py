@@ -67,7 +67,8 @@ class CollectiveFingerprint(Comm):
     the world communicator (and every communicator split from it)."""
 
     _CHECKED = ("all_reduce", "reduce", "broadcast", "all_gather_into_tensor",
-                "reduce_scatter_tensor", "bcast", "allgather", "barrier", "split", "scatter")
+                "reduce_scatter_tensor", "bcast", "allgather", "barrier", "split", "scatter",
+                "all_to_all_v")
 
     def __init__(self, comm):
         object.__setattr__(self, "_comm", comm)

@@ -22,6 +22,10 @@ def _worker(rank, size, port, fn, args, q):
                        "WORLD_SIZE": str(size), "LOCAL_RANK": str(rank),
                        "MULTIGRAD_DEVICE_COMM": "0", "MULTIGRAD_PROGRESS": "0",
                        "OMP_NUM_THREADS": "1"})
+    # the engines' setup-time re-partition by parameter owner is on by default for several
+    # ranks; tests of the data-parallel (hashed) schedules keep their placement, the
+    # re-partition tests turn it back on (tests/test_repartition.py)
+    os.environ.setdefault("MULTIGRAD_REPARTITION", "0")
     try:
         import torch
         torch.set_num_threads(1)

@@ -226,10 +226,14 @@ def test_bench_self_launches_n_ranks():
     assert len(lines) == 1, r.stdout
     rec = lines[0]
     assert rec["n_gpus"] == 2 and rec["value"] > 0
-    assert rec["config"]["placement"] == "hashed"
-    assert rec["config"]["optimizer_sharding"] == "zero1"
-    assert rec["owner_steps_per_s"] > 0
-    assert rec["owner_config"]["optimizer_sharding"] == "owner"
+    # value: the hashed input re-partitioned by parameter owner at setup (one all-to-all-v)
+    assert rec["config"]["placement"].startswith("owner (re-partitioned")
+    assert rec["config"]["optimizer_sharding"] == "owner"
+    assert rec["repartition"]["halos_after"] > 0 and rec["repartition"]["total_s"] >= 0
+    # dense_steps_per_s: the same input, dense gradient summed across ranks every step
+    assert rec["dense_steps_per_s"] > 0
+    assert rec["dense_config"]["optimizer_sharding"] == "zero1"
+    assert rec["dense_config"]["loss_last"] == pytest.approx(rec["loss_last"], rel=1e-4)
 
 
 def test_bench_launcher_parent_is_gpu_free():

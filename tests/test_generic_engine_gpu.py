@@ -137,6 +137,7 @@ def test_captured_evaluator_drives_scipy_bfgs(monkeypatch):
     data = make_docs_data()
     model = DocsSMFModel(aux_data=data)
     init = torch.tensor([-3.5, 0.2])
+    monkeypatch.setenv("MULTIGRAD_SMF2", "0")  # the generic captured evaluator (not the fused step)
     monkeypatch.setenv("MULTIGRAD_GENERIC_ENGINE", "0")
     ref = model.run_bfgs(init, method="scipy")
     monkeypatch.setenv("MULTIGRAD_GENERIC_ENGINE", "1")
@@ -148,6 +149,7 @@ def test_captured_evaluator_drives_scipy_bfgs(monkeypatch):
 
 def _bfgs_two(rank, size, engine):
     os.environ["MULTIGRAD_GENERIC_ENGINE"] = "1" if engine else "0"
+    os.environ["MULTIGRAD_SMF2"] = "0"  # the generic captured evaluator (not the fused step)
     import multigrad_amd as mg
     from multigrad_amd.models.smf import DocsSMFModel, make_docs_data
     comm = mg.get_world_comm()

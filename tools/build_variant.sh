@@ -4,6 +4,7 @@
 set -eu
 R=$(cd "$(dirname "$0")/.." && pwd)
 name=$1; shift
-mkdir -p "$R/variants/$name"
+D=${VARIANT_DIR:-$R/variants}
+mkdir -p "$D/$name"
 MULTIGRAD_HIPCC_FLAGS="$*" MULTIGRAD_OBJ_DIR="$R/build/variants/$name" \
-  MULTIGRAD_TARGET="$R/variants/$name/_C.so" python -m multigrad_amd.ops.build
+  MULTIGRAD_TARGET="$D/$name/_C.so" python -m multigrad_amd.ops.build
