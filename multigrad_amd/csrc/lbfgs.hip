@@ -137,13 +137,14 @@ __global__ __launch_bounds__(kDotThreads) void multi_dot_reduce_kernel(
   if (threadIdx.x == 0) out[t] = s[0];
 }
 
-// y = alpha * x + sum_i coef[i] * H[i, :]   (coef in device memory, nrows <= 64)
+// y = alpha * x + sum_i coef[i] * H[i, :]   (coef in device memory, nrows <= kLincombRows)
+constexpr int kLincombRows = 256;
 __global__ __launch_bounds__(256) void lincomb_kernel(const float* __restrict__ H, int64_t ldh,
                                                       int nrows, const float* __restrict__ coef,
                                                       float alpha, const float* __restrict__ x,
                                                       int64_t n, float* __restrict__ y) {
-  __shared__ float c[64];
-  if (threadIdx.x < nrows) c[threadIdx.x] = coef[threadIdx.x];
+  __shared__ float c[kLincombRows];
+  for (int i = threadIdx.x; i < nrows; i += blockDim.x) c[i] = coef[i];
   __syncthreads();
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += stride) {
@@ -261,7 +262,7 @@ void lincomb(torch::Tensor H, int64_t nrows, torch::Tensor coef, double alpha,
   TORCH_CHECK(H.is_cuda() && coef.is_cuda() && y.is_cuda(), "device tensors");
   TORCH_CHECK(H.scalar_type() == at::kFloat && coef.scalar_type() == at::kFloat &&
               y.scalar_type() == at::kFloat, "fp32");
-  TORCH_CHECK(H.dim() == 2 && H.stride(1) == 1 && nrows <= H.size(0) && nrows <= 64 &&
+  TORCH_CHECK(H.dim() == 2 && H.stride(1) == 1 && nrows <= H.size(0) && nrows <= kLincombRows &&
               coef.numel() >= nrows && n <= H.size(1) && y.numel() >= n, "bad shapes");
   const float* xp = nullptr;
   if (x.has_value() && x->defined()) {

@@ -930,11 +930,11 @@ __device__ __forceinline__ EmLane em_lane(float inv, float delta) {
 // constants come as scalars, not as the EmLane struct: splats of adjacent struct fields were
 // widened into 8-byte loads that kept (a1, a3, a5) in private memory, a scratch store and two
 // scratch loads at every group start of the headline kernel.
-template <int NB, bool RESID>
+template <int NB, bool RESID, bool A7 = false>
 __device__ __forceinline__ void em_halo(float nm, float inv, float dw4, float a1, float a3,
                                         float a5, const SmfBins& b,
                                         v2f (&F)[EdgePairs<NB>::NV], v2f (&Wa)[EdgePairs<NB>::NV],
-                                        v2f (&E)[EdgePairs<NB>::NV]) {
+                                        v2f (&E)[EdgePairs<NB>::NV], float a7 = 0.0f) {
   using EP = EdgePairs<NB>;
   constexpr int M = EP::NP / 2;
   // sentinel / masked halos (x = -1e30 or -inf): f = 0, and w^4 stays finite so 0 * E = 0
@@ -955,7 +955,13 @@ __device__ __forceinline__ void em_halo(float nm, float inv, float dw4, float a1
     F[i] = F[i] + p;
     if constexpr (RESID) Wa[i] = Wa[i] + pw;
     const v2f w2 = w * w;
-    v2f t = w2 * a5 + a3;
+    v2f t;
+    if constexpr (A7) {
+      t = w2 * a7 + a5;
+      t = t * w2 + a3;
+    } else {
+      t = w2 * a5 + a3;
+    }
     t = t * w2 + a1;
     E[i] = pw * t + E[i];
   };
@@ -979,7 +985,8 @@ __device__ __forceinline__ void em_halo(float nm, float inv, float dw4, float a1
     F[EP::NP].x += pz;
     if constexpr (RESID) Wa[EP::NP].x += pw;
     const float w2 = wz * wz;
-    const float t = fmaf(fmaf(w2, a5, a3), w2, a1);
+    const float t = A7 ? fmaf(fmaf(fmaf(w2, a7, a5), w2, a3), w2, a1)
+                       : fmaf(fmaf(w2, a5, a3), w2, a1);
     E[EP::NP].x = fmaf(pw, t, E[EP::NP].x);
   }
   if constexpr (M > 0) {
@@ -1043,8 +1050,8 @@ __device__ __forceinline__ void lane_halo_exact1(float x, float ninv, float mua,
 // End of a group: apply the lane constants Q_j to the pair sums (F, Wa become the true
 // residuals G, W), and add the lane's cumulative bin masses C_e (C_{k+1} - C_k = mass_k) to
 // the per-edge accumulators of the edge-pair path.
-template <int NB>
-__device__ __forceinline__ void em_group_end(const EmLane& L, v2f (&F)[EdgePairs<NB>::NV],
+template <int NB, class LaneT>
+__device__ __forceinline__ void em_group_end(const LaneT& L, v2f (&F)[EdgePairs<NB>::NV],
                                              v2f (&Wa)[EdgePairs<NB>::NV],
                                              v2f (&E)[EdgePairs<NB>::NV],
                                              v2f (&accp)[EdgePairs<NB>::NV]) {
@@ -2882,6 +2889,76 @@ struct S2 {
   static constexpr int R = 3 * NB + 2;   // values per rank and step: masses, G, W
 };
 
+// The shared-parameter step's Euler-Maclaurin sums carry one more correction term than the
+// lanes forward's (B_8: f^(7) = -He_7 f, He_7 = z^7 - 21 z^5 + 105 z^3 - 105 z), so
+//   E(z) = f z (c1 + c3 z^2 + c5 z^4 + c7 z^6) with, on top of the three-term constants,
+//   c1 += 105 h^8/1209600, c3 -= 105 h^8/1209600, c5 += 21 h^8/1209600, c7 = -h^8/1209600.
+// The remainder becomes h^11 B_10/10! max|f^(10)|/sqrt(2 pi) = 7.9e-6 h^11: 1.6e-7 at h = 0.7,
+// the absolute contract of the per-edge tails (normal_tail_parts_w, 1.6e-7) -- so the fast
+// path covers sigma >= delta / 0.7 instead of delta / 0.5 (the reference's test model fits
+// sigma = 0.2 at delta = 0.1: h = 0.5, on the old boundary) for ~6 more packed ops per halo.
+constexpr float kEmHMax2 = 0.7f;
+
+struct EmLane7 {
+  float inv, dw4, a1, a3, a5, a7;
+};
+
+__device__ __forceinline__ EmLane7 em_lane7(float inv, float delta) {
+  constexpr float ik = 1.0f / kWScale;
+  EmLane7 L;
+  L.inv = inv;
+  const float dw = delta * inv;
+  L.dw4 = -4.0f * dw;
+  const float h = dw * ik;
+  const float h2 = h * h, h4 = h2 * h2, h6 = h4 * h2, h8 = h4 * h4;
+  const float ik2 = ik * ik;
+  L.a1 = (h2 * (1.0f / 12.0f) + h4 * (3.0f / 720.0f) + h6 * (15.0f / 30240.0f) +
+          h8 * (105.0f / 1209600.0f)) * ik;
+  L.a3 = -(h4 * (1.0f / 720.0f) + h6 * (10.0f / 30240.0f) + h8 * (105.0f / 1209600.0f)) * (ik * ik2);
+  L.a5 = (h6 * (1.0f / 30240.0f) + h8 * (21.0f / 1209600.0f)) * (ik * ik2 * ik2);
+  L.a7 = -h8 * (1.0f / 1209600.0f) * (ik * ik2 * ik2 * ik2);
+  return L;
+}
+
+template <int NB>
+__device__ __forceinline__ float pair_edge(const v2f (&P)[EdgePairs<NB>::NV], int e);
+
+// End of the shared-parameter EM sums: the lane constants Q_j applied to F, Wa, E (as
+// em_group_end), then the bin masses formed DIRECTLY per bin,
+//   mass_k = (h/2)(f_k + f_{k+1}) + E_{k+1} - E_k      (over sqrt(2 pi)),
+// not as differences of cumulative masses: the shared-parameter bins span many decades
+// (the docs model: 431 halos' worth in the first bin, 3e-4 in the last at sigma = 0.19), and
+// a float32 cumulative sum of the large bins' mass would cancel the small bins' away.
+template <int NB>
+__device__ __forceinline__ void em2_finish(const EmLane7& L, v2f (&F)[EdgePairs<NB>::NV],
+                                           v2f (&Wa)[EdgePairs<NB>::NV],
+                                           v2f (&E)[EdgePairs<NB>::NV],
+                                           float (&out)[S2<NB>::R]) {
+  using EP = EdgePairs<NB>;
+  constexpr int M = EP::NP / 2;
+  const float l4 = 0.25f * L.dw4 * L.dw4;
+#pragma unroll
+  for (int i = 0; i < EP::NV; ++i) {
+    const int j = i - M;
+    v2f Q;
+    Q.x = (j * (j - 1) == 0) ? 1.0f : fast_exp2(-l4 * (float)(j * (j - 1)));
+    Q.y = (i == EP::NP) ? Q.x : ((j * j == 0) ? 1.0f : fast_exp2(-l4 * (float)(j * j)));
+    F[i] = F[i] * Q;
+    Wa[i] = Wa[i] * Q;
+    E[i] = E[i] * Q;
+  }
+  const float hh = (-0.125f / kWScale) * L.dw4;  // h / 2
+#pragma unroll
+  for (int k = 0; k < NB; ++k)
+    out[k] = kInvSqrt2Pi * fmaf(hh, pair_edge<NB>(F, k) + pair_edge<NB>(F, k + 1),
+                                pair_edge<NB>(E, k + 1) - pair_edge<NB>(E, k));
+#pragma unroll
+  for (int e = 0; e <= NB; ++e) {
+    out[NB + e] = pair_edge<NB>(F, e);
+    out[2 * NB + 1 + e] = pair_edge<NB>(Wa, e);
+  }
+}
+
 // halos per thread per round of the forward loop (loads of the next round in flight)
 #ifndef MG_S2_AHEAD
 #define MG_S2_AHEAD 2
@@ -2971,9 +3048,9 @@ __device__ __forceinline__ void smf2_accumulate(const float* __restrict__ x, int
     }
   };
   const int64_t step = (int64_t)kS2Ahead * stride;
-  // EM range: uniform unpadded bins and h = delta / sigma <= kEmHMax (a uniform branch)
-  if (b.delta > 0.0f && b.delta * isig <= kEmHMax) {
-    const EmLane L = em_lane(inv, b.delta);
+  // EM range: uniform unpadded bins and h = delta / sigma <= kEmHMax2 (a uniform branch)
+  if (b.delta > 0.0f && b.delta * isig <= kEmHMax2) {
+    const EmLane7 L = em_lane7(inv, b.delta);
     const float nma = -a * inv;
     v2f E[EP::NV];
 #pragma unroll
@@ -2985,11 +3062,13 @@ __device__ __forceinline__ void smf2_accumulate(const float* __restrict__ x, int
       ld(w0 + step, xb);
 #pragma unroll
       for (int u = 0; u < kS2Ahead; ++u) {
-        em_halo<NB, true>(fmaf(xa[u], -L.inv, nma), L.inv, L.dw4, L.a1, L.a3, L.a5, b, G, W, E);
+        em_halo<NB, true, true>(fmaf(xa[u], -L.inv, nma), L.inv, L.dw4, L.a1, L.a3, L.a5, b, G, W,
+                                E, L.a7);
         xa[u] = xb[u];
       }
     }
-    em_group_end<NB>(L, G, W, E, acc);   // G, W become the residuals; acc the cumulative C_e
+    em2_finish<NB>(L, G, W, E, out);   // G, W become the residuals; the masses per bin
+    return;
   } else {
     const float ninv = -inv, mua = a * inv;
     float xa[kS2Ahead];
@@ -3024,11 +3103,11 @@ __device__ __forceinline__ void smf2_accumulate(const float* __restrict__ x, int
 // advanced by thread 0 unless evaluating.
 template <int NB, bool LOGSIG>
 __device__ __forceinline__ void smf2_finish(const Smf2Step& P, const SmfBins& b, float* vals,
-                                            unsigned* seq, float* thn) {
+                                            unsigned* seq, float* thn, int size) {
   constexpr int R = S2<NB>::R;
   __shared__ float g[kMaxBins];
   __shared__ float d2[kMaxBins];
-  if (P.size > 1) xgmi_block_allreduce(P.peers, P.rank, P.size, vals, R, seq, P.err, P.ticks);
+  if (size > 1) xgmi_block_allreduce(P.peers, P.rank, size, vals, R, seq, P.err, P.ticks);
   const int k = threadIdx.x;
   const int nb = P.nb;
   if (k < nb) {
@@ -3074,6 +3153,7 @@ __device__ __forceinline__ void smf2_finish(const Smf2Step& P, const SmfBins& b,
         const float gg[2] = {gr.x, gr.y};
         const float po[2] = {th.x, th.y};
         float pn[2];
+#pragma unroll
         for (int j = 0; j < 2; ++j) {
           float uu = P.u[j], mm = P.m[j], vv = P.v[j];
           if (P.bounded) {
@@ -3168,7 +3248,7 @@ __device__ __forceinline__ void vmem_wait_n() {  // s_waitcnt vmcnt(N), expcnt /
 // measured 400 us per 1e8 halos (4 waves / SIMD at 102 VGPRs: the loads were not covered).
 template <int NB>
 __device__ __forceinline__ void smf2_em_staged(const float* __restrict__ x, int64_t n,
-                                               const EmLane& L, float nma, const SmfBins& b,
+                                               const EmLane7& L, float nma, const SmfBins& b,
                                                float* tiles, v2f (&G)[EdgePairs<NB>::NV],
                                                v2f (&W)[EdgePairs<NB>::NV],
                                                v2f (&E)[EdgePairs<NB>::NV]) {
@@ -3200,7 +3280,8 @@ __device__ __forceinline__ void smf2_em_staged(const float* __restrict__ x, int6
       const int64_t i = t * TH + r * kWave + lane;
       float xv = cur[r * kWave + lane];
       xv = i < n ? xv : kLaneSentinel;
-      em_halo<NB, true>(fmaf(xv, -L.inv, nma), L.inv, L.dw4, L.a1, L.a3, L.a5, b, G, W, E);
+      em_halo<NB, true, true>(fmaf(xv, -L.inv, nma), L.inv, L.dw4, L.a1, L.a3, L.a5, b, G, W, E,
+                              L.a7);
     }
   }
 }
@@ -3217,22 +3298,15 @@ __global__ __launch_bounds__(kThreads) void smf2_fwd_kernel(const float* __restr
   const int lane = threadIdx.x & (kWave - 1);
   float v[R];
   const float isig = inv_sigma<LOGSIG>(s);
-  if (b.delta > 0.0f && b.delta * isig <= kEmHMax) {
+  if (b.delta > 0.0f && b.delta * isig <= kEmHMax2) {
     const float inv = isig * kWScale;
-    const EmLane L = em_lane(inv, b.delta);
+    const EmLane7 L = em_lane7(inv, b.delta);
     v2f acc[EP::NV], G[EP::NV], W[EP::NV], E[EP::NV];
 #pragma unroll
     for (int i = 0; i < EP::NV; ++i) acc[i] = G[i] = W[i] = E[i] = (v2f)(0.0f);
     smf2_em_staged<NB>(x, n, L, -a * inv, b, tiles + (threadIdx.x >> 6) * 2 * kS2Rows * kWave,
                        G, W, E);
-    em_group_end<NB>(L, G, W, E, acc);
-#pragma unroll
-    for (int k = 0; k < NB; ++k) v[k] = pair_edge<NB>(acc, k + 1) - pair_edge<NB>(acc, k);
-#pragma unroll
-    for (int e = 0; e <= NB; ++e) {
-      v[NB + e] = pair_edge<NB>(G, e);
-      v[2 * NB + 1 + e] = pair_edge<NB>(W, e);
-    }
+    em2_finish<NB>(L, G, W, E, v);
   } else {
     const int64_t first = (int64_t)blockIdx.x * kThreads + (threadIdx.x - lane);
     const S2Out<NB> o = smf2_edge_pass<NB, LOGSIG>(x, first, n, (int64_t)gridDim.x * kThreads,
@@ -3276,9 +3350,8 @@ __global__ __launch_bounds__(kEpiThreads) void smf2_step_kernel(const float* __r
       return;
     }
   }
-  Smf2Step Q = P;
-  if (mode == 2) Q.size = 1;  // already summed across ranks
-  smf2_finish<NB, LOGSIG>(Q, b, vals, P.seq, nullptr);
+  // mode 2: the sums are already global
+  smf2_finish<NB, LOGSIG>(P, b, vals, P.seq, nullptr, mode == 2 ? 1 : P.size);
 }
 
 // Persistent schedule: ONE workgroup of kS2LoopThreads runs `steps` whole optimizer steps
@@ -3307,7 +3380,7 @@ __global__ __launch_bounds__(kS2LoopThreads) void smf2_loop_kernel(const float* 
     float v[R];
     smf2_accumulate<NB, LOGSIG>(x, first, n, (int64_t)kS2LoopThreads, th[0], th[1], b, v);
     block_sum_par<R>(v, scratch, vals);
-    smf2_finish<NB, LOGSIG>(P, b, vals, &seq_sh, th);
+    smf2_finish<NB, LOGSIG>(P, b, vals, &seq_sh, th, P.size);
   }
   if (threadIdx.x == 0 && P.size > 1) *P.seq = seq_sh;
 }

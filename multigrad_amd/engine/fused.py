@@ -88,6 +88,19 @@ def _side_stream_mode() -> str:
     return "auto"
 
 
+def _autotune_mode() -> str:
+    """``MULTIGRAD_AUTOTUNE``: ``auto`` (default) -- the setup autotune and the settle steps
+    get at most ``MULTIGRAD_TUNE_BUDGET`` (0.1) of the requested run's estimated time, and a
+    run too short for the minimum windows keeps the default schedule (the first candidate);
+    ``on`` -- always the full autotune (bench.py); ``off`` -- never."""
+    v = os.environ.get("MULTIGRAD_AUTOTUNE", "auto").strip().lower()
+    if v in ("0", "off", "false", "no"):
+        return "off"
+    if v in ("1", "on", "true", "yes", "full"):
+        return "on"
+    return "auto"
+
+
 def _best_ms(tuning) -> float:
     """Fastest measured candidate of an autotune record (dropped candidates have no time)."""
     ms = [c["ms"] for c in tuning["candidates"] if c.get("ms") is not None]
@@ -170,6 +183,15 @@ class FusedAdamEngine:
             r = self.size > 1 and self.allow_owner and z is None
         self.repartition = bool(r) and self.size > 1 and self.allow_owner
         self.repartitioned = None  # the model's re-partition record, once done
+        # kept across setup() calls of this engine (a model's cached engine serves every
+        # run_* call, models/population.py fused_engine): device buffers of the same shape,
+        # the autotune verdicts and -- when every buffer and scalar a graph captured is
+        # unchanged -- the captured graphs (the analogue of JAX's jit cache)
+        self._bufs = {}
+        self._tune_cache = {}
+        self._gkey = None
+        self.stats = {"setups": 0, "captures": 0, "trial_steps": 0, "layouts": 0}
+        self.closed = False
         self.fuse_vjp_adam = bool(_env_flag("MULTIGRAD_FUSED_VJP_ADAM", True))
         # slab reduction (+ one-shot cross-rank sum) + loss in one launch
         self.fuse_epilogue = bool(_env_flag("MULTIGRAD_FUSED_EPILOGUE", True))
@@ -209,6 +231,17 @@ class FusedAdamEngine:
         # --profile-phases); never active inside a graph capture
         self.timer = PhaseTimer()
 
+    def _buf(self, name: str, shape, dtype=torch.float32) -> torch.Tensor:
+        """A zeroed device buffer, the one of the previous setup when the shape matches."""
+        shape = tuple(int(v) for v in (shape if isinstance(shape, (tuple, list)) else (shape,)))
+        t = self._bufs.get(name)
+        if t is None or tuple(t.shape) != shape or t.dtype != dtype or t.device != self.device:
+            t = torch.zeros(shape, dtype=dtype, device=self.device)
+            self._bufs[name] = t
+        else:
+            t.zero_()
+        return t
+
     # ------------------------------------------------------------------ stream
     def _engine_stream(self):
         dev = getattr(self, "device", None)
@@ -246,10 +279,15 @@ class FusedAdamEngine:
                   eps=eps, history=history, legacy_bounds_jacobian=legacy_bounds_jacobian)
         self._chunks_override = None
         self._maybe_repartition()
+        ck = ("chunks", self.size, bool(param_bounds is None), history == "full")
+        if ck in self._tune_cache and not self._chunks_explicit:
+            # the chunk count this engine measured before (hashed two-shot schedule)
+            self._chunks_override = self._tune_cache[ck]
         self._setup(guess, nsteps, **kw)
         tun = self.tuning
         if not (tun and self.twoshot is not None and not self.owner and self.C == 2
-                and not self._chunks_explicit and "ts_side" in tun["chosen"]):
+                and not self._chunks_explicit and "ts_side" in tun["chosen"]
+                and not tun.get("budget_skipped") and not tun.get("cached")):
             return self
         t2 = _best_ms(tun)
         skip = getattr(self, "_skip_autotune", False)
@@ -299,6 +337,7 @@ class FusedAdamEngine:
                 setattr(self, k, v)
             self.graph = None
         self.tuning = dict(tuned[best], chunks=dict(chunk_times, chosen=best))
+        self._tune_cache[ck] = best
         dropped = [dict(d, chunks=n) for n, t in tuned.items() for d in t.get("dropped", [])]
         if dropped:  # candidates dropped in any of the chunk-count tunings, with the reason
             self.tuning["dropped"] = dropped
@@ -336,10 +375,16 @@ class FusedAdamEngine:
             if self.twoshot is None:
                 ub, pb, P_pad, lengths = plan_chunks(J, upp, W, self.nchunks_req)
         hint = getattr(md, "engine_layout_hint", None)
+        changed = True
         if hint is not None:  # e.g. lanes grouped by forward path at the starting point
-            hint(guess)
-        trace(f"engine: layout ({'owner' if self.owner else 'dense'}, {len(ub) - 1} chunks)")
-        md.engine_set_chunks(ub)
+            changed = bool(hint(guess))
+        cur = getattr(md, "engine_chunks_current", None)
+        if changed or cur is None or not cur(ub):
+            # (a model that reports its current chunks keeps its layout when neither the
+            # chunks nor the layout classes changed: no rebuild on a repeated run)
+            trace(f"engine: layout ({'owner' if self.owner else 'dense'}, {len(ub) - 1} chunks)")
+            md.engine_set_chunks(ub)
+            self.stats["layouts"] += 1
         self._ub = list(ub)
         if self.size > 1 and dev.type == "cuda" and self.fuse_epilogue:
             from ..parallel.xgmi import get_oneshot
@@ -370,6 +415,10 @@ class FusedAdamEngine:
                             torch.cat([bounds.hi, torch.full((pad,), math.inf, **f32)]),
                             torch.cat([bounds.kind, torch.full((pad,), KIND_NONE, dtype=torch.int8,
                                                                device=dev)]))
+        old_b = getattr(self, "bounds", None)
+        if bounds is not None and old_b is not None and bounds.lo.shape == old_b.lo.shape and \
+                torch.equal(bounds.lo, old_b.lo) and torch.equal(bounds.hi, old_b.hi):
+            bounds = old_b  # the same box: the same tensors (graphs captured on them stay valid)
         self.bounds = bounds
         if self.twoshot is not None:
             # parameters and gradient live in the exported peer-memory regions
@@ -378,27 +427,27 @@ class FusedAdamEngine:
             self.grad = self.twoshot.grad
             self.grad.zero_()
         else:
-            theta = torch.zeros(P_pad, **f32)
+            theta = self._buf("theta", P_pad)
         theta[:P] = p0
         if bounds is not None:  # the recorded start is T^-1(T(guess)), as the reference
             theta.copy_(bounds.inverse(bounds.forward(theta)))
         self.theta = theta
         if self.twoshot is None:
-            self.grad = torch.zeros(P_pad, **f32)
+            self.grad = self._buf("grad", P_pad)
         nS = md.engine_nS()
         self.nS = nS
         self.rows = [md.engine_fwd_rows(c) for c in range(self.C)]
-        self.S = torch.zeros(nS, **f32)
-        self.slab = torch.zeros(max(1, sum(self.rows)) * nS, **f32)
-        self.h = torch.zeros(nS + 1, **f32)
-        self.loss = torch.zeros(1, **f32)
-        self.step_dev = torch.zeros((self.C, 2), dtype=torch.int32, device=dev)
+        self.S = self._buf("S", nS)
+        self.slab = self._buf("slab", max(1, sum(self.rows)) * nS)
+        self.h = self._buf("h", nS + 1)
+        self.loss = self._buf("loss", 1)
+        self.step_dev = self._buf("step_dev", (self.C, 2), torch.int32)
         if self.owner:
             a, b = pb[self.rank], pb[self.rank + 1]
             self.own_range = (a, b)
             n = b - a
-            self.m = torch.zeros(n, **f32)
-            self.v = torch.zeros(n, **f32)
+            self.m = self._buf("m", n)
+            self.v = self._buf("v", n)
             if bounds is not None:
                 self.bounds_loc = Bounds(bounds.lo[a:b].contiguous(), bounds.hi[a:b].contiguous(),
                                          bounds.kind[a:b].contiguous())
@@ -412,9 +461,9 @@ class FusedAdamEngine:
             nloc = sum(self.loc_len)
             self.own = [(pb[c] + self.rank * self.loc_len[c], pb[c] + (self.rank + 1) * self.loc_len[c])
                         for c in range(self.C)]
-            self.m = torch.zeros(nloc, **f32)
-            self.v = torch.zeros(nloc, **f32)
-            self.g_loc = torch.zeros(nloc, **f32)
+            self.m = self._buf("m", nloc)
+            self.v = self._buf("v", nloc)
+            self.g_loc = self._buf("g_loc", nloc)
             if bounds is not None:
                 idx = torch.cat([torch.arange(a, b, device=dev) for a, b in self.own])
                 self.bounds_loc = Bounds(bounds.lo[idx].contiguous(), bounds.hi[idx].contiguous(),
@@ -424,24 +473,31 @@ class FusedAdamEngine:
                 self.bounds_loc = None
                 self.u_loc = None
         else:
-            self.u = bounds.forward(theta).contiguous() if bounds is not None else theta
-            self.m = torch.zeros(P_pad, **f32)
-            self.v = torch.zeros(P_pad, **f32)
+            if bounds is not None:
+                self.u = self._buf("u", P_pad)
+                self.u.copy_(bounds.forward(theta))
+            else:
+                self.u = theta
+            self.m = self._buf("m", P_pad)
+            self.v = self._buf("v", P_pad)
         self.step_host = 0
         self.nsteps = int(nsteps)
         sharded = self.zero or self.owner
-        self.history = History(history if not (sharded and history == "full") else "last",
-                               nsteps, theta[:P].detach().clone())
+        hmode = history if not (sharded and history == "full") else "last"
+        self.history = History(hmode, nsteps, theta[:P].detach().clone(),
+                               buf=self._bufs.get("history") if hmode == "full" else None)
+        if hmode == "full":
+            self._bufs["history"] = self.history.buf
         self.traj_loc = None
         self.history_mode = history
         if self.owner:
             if history == "full":
                 a, b = self.own_range
-                self.traj_loc = torch.zeros((self.nsteps + 1, b - a), **f32)
+                self.traj_loc = self._buf("traj_loc", (self.nsteps + 1, b - a))
                 self.traj_loc[0] = theta[a:b]
         elif self.zero:
             if history == "full":
-                self.traj_loc = torch.zeros((self.nsteps + 1, sum(self.loc_len)), **f32)
+                self.traj_loc = self._buf("traj_loc", (self.nsteps + 1, sum(self.loc_len)))
                 for c in range(self.C):
                     a, b = self.own[c]
                     o, n = self.loc_off[c], self.loc_len[c]
@@ -513,7 +569,10 @@ class FusedAdamEngine:
             self.use_graph = self.capturable and not self.pipeline and self.size == 1
         elif self.use_graph and not self.capturable:
             self.use_graph = False  # e.g. RCCL collectives in the step: eager launches
-        self.graph = None
+        gk = self._graph_key()
+        if gk != self._gkey:  # a buffer or scalar the captured graphs baked in changed
+            self.graph = None
+            self._gkey = gk
         self.tuning = None
         self._tuning = False
         self._relayout_init()
@@ -541,11 +600,31 @@ class FusedAdamEngine:
             cands = [{"use_graph": False}, {"use_graph": True, "graph_steps": 1}]
             if self.graph_steps > 1 and (self.history.mode == "full" or self.traj_loc is not None):
                 cands.append({"use_graph": True, "graph_steps": self.graph_steps})
-        if cands and dev.type == "cuda" and _env_flag("MULTIGRAD_AUTOTUNE", True) and \
+        self.stats["setups"] += 1
+        if cands and dev.type == "cuda" and _autotune_mode() != "off" and \
                 not getattr(self, "_skip_autotune", False):
             self._autotune(cands, min_window_s=1e-3 * float(
                 os.environ.get("MULTIGRAD_AUTOTUNE_WINDOW_MS", "30")))
         return self
+
+    def _graph_key(self):
+        """Everything a captured step bakes in: the identity of every buffer it reads or
+        writes and the launch scalars.  Equal keys across setups keep the graphs."""
+        ids = [id(getattr(self, n, None)) for n in (
+            "theta", "grad", "S", "slab", "h", "loss", "step_dev", "m", "v", "u", "g_loc",
+            "traj_loc", "u_loc", "oneshot", "twoshot")]
+        for b in (getattr(self, "bounds", None), getattr(self, "bounds_loc", None)):
+            ids += [None] if b is None else [id(b.lo), id(b.hi), id(b.kind)]
+        hist = getattr(self, "history", None)
+        ids.append(id(getattr(hist, "buf", None)) if hist is not None else None)
+        epoch = getattr(self.model, "engine_layout_epoch", None)
+        return (tuple(ids), self.lr, self.b1, self.b2, self.eps, self.legacy, self.pipeline,
+                self.owner, self.zero, self.C, None if epoch is None else epoch())
+
+    def _tune_key(self, cands):
+        return (tuple(tuple(sorted(c.items())) for c in cands), self.P, self.size, self.owner,
+                self.zero, self.pipeline, self.C, self.history.mode == "full",
+                self.traj_loc is not None, self.bounds is None)
 
     @staticmethod
     def _param_order(md, P: int, upp: int, dev):
@@ -727,11 +806,28 @@ class FusedAdamEngine:
         return self.history.buf.reshape(-1)
 
     def _autotune(self, cands, warm: int = 2, min_window_s: float = 0.008, **kw):
+        key = self._tune_key(cands)
+        hit = self._tune_cache.get(key)
+        if hit is not None:
+            # this engine timed these candidates before (a repeated run_* call): no trial
+            # steps, the verdict is applied as it is
+            changed = False
+            for k, v in hit["chosen"].items():
+                if getattr(self, k, None) != v:
+                    setattr(self, k, v)
+                    changed = True
+            if changed:
+                self.graph = None
+            self.tuning = dict(hit, cached=True)
+            trace(f"engine: autotune verdict cached {hit['chosen']}")
+            return
         trace(f"engine: autotune {cands}")
         try:
-            return self._autotune_impl(cands, warm, min_window_s, **kw)
+            self._autotune_impl(cands, warm, min_window_s, **kw)
         finally:
             trace(f"engine: autotune done {getattr(self, 'tuning', None)}")
+        if self.tuning is not None and not self.tuning.get("budget_skipped"):
+            self._tune_cache[key] = {k: v for k, v in self.tuning.items() if k != "cached"}
 
     def _autotune_impl(self, cands, warm: int = 2, min_window_s: float = 0.008,
                   max_reps: int = 400):
@@ -814,6 +910,27 @@ class FusedAdamEngine:
             why = verdict(cands[0])
             if why is not None:  # the probe of the first candidate already failed
                 dropped.append(dict(cands[0], reason=why))
+            self.stats["trial_steps"] += warm + 2
+            rounds_b = max(1, int(os.environ.get("MULTIGRAD_AUTOTUNE_ROUNDS", "2")))
+            budget_s = None
+            if _autotune_mode() == "auto":
+                # at most MULTIGRAD_TUNE_BUDGET of the requested run (est: the slowest rank's
+                # step, identical on every rank, so every rank takes the same branch)
+                budget_s = float(os.environ.get("MULTIGRAD_TUNE_BUDGET", "0.1")) * est * \
+                    max(1, self.nsteps)
+                extra = warm + (self.graph_steps if any(c.get("use_graph") for c in cands) else 0)
+                fit = int(budget_s / max(est, 1e-9) / (len(cands) * rounds_b)) - extra
+                if fit < 8 and why is None:
+                    apply(cands[0])
+                    self.tuning = {"chosen": cands[0], "budget_skipped": True,
+                                   "budget_ms": round(1e3 * budget_s, 3),
+                                   "step_ms_probe": round(1e3 * est, 4)}
+                    self._settle(est, restore, budget_s=budget_s)
+                    if multi:
+                        torch.cuda.synchronize()
+                        self.comm.barrier()
+                    return
+                reps = max(8, min(reps, fit))
             times = [math.inf] * len(cands)
             # MULTIGRAD_AUTOTUNE_ROUNDS (2) rounds, the order reversed every other round, the
             # best window of each candidate kept: a single pass in a fixed order let the
@@ -837,6 +954,7 @@ class FusedAdamEngine:
                     if self._block_ok():
                         self._run_steps(self.graph_steps)  # capture (and first replay) untimed
                     t = window(reps)
+                    self.stats["trial_steps"] += warm + reps
                     self._fault_c = None
                     restore()
                     why = verdict(c)
@@ -886,12 +1004,13 @@ class FusedAdamEngine:
             if self._block_ok():
                 self._capture(self.graph_steps)
             self.pending = pend
-        self._settle(est, restore)
+        used = rounds * len(cands) * (reps + warm) * est
+        self._settle(est, restore, budget_s=None if budget_s is None else max(0.0, budget_s - used))
         if multi:
             torch.cuda.synchronize()
             self.comm.barrier()
 
-    def _settle(self, step_s: float, restore) -> None:
+    def _settle(self, step_s: float, restore, budget_s: Optional[float] = None) -> None:
         """End the setup with ``MULTIGRAD_SETTLE_MS`` (60) of eager steps (no trajectory
         rows; the optimizer state is restored afterwards), so the first real steps do not
         start from an idle GPU.  Measured on one MI355X (profiles/narrow_sweep/README.md):
@@ -900,9 +1019,12 @@ class FusedAdamEngine:
         -- the power controller's transient after an idle gap; a 20-step timing from there
         measured ~1850 steps/s against ~2250 in steady state."""
         ms = float(os.environ.get("MULTIGRAD_SETTLE_MS", "60"))
-        if ms <= 0 or self.device.type != "cuda":
+        if budget_s is not None:  # MULTIGRAD_AUTOTUNE=auto: what is left of the tuning budget
+            ms = min(ms, 1e3 * budget_s)
+        if ms <= 0 or self.device.type != "cuda" or (budget_s is not None and ms < 1e3 * step_s):
             return
         n = int(min(2000, max(1, math.ceil(1e-3 * ms / max(step_s, 1e-5)))))
+        self.stats["trial_steps"] += n
         use_graph = self.use_graph
         self._tuning = True
         self.use_graph = False  # eager launches: the captured graphs write trajectory rows
@@ -948,6 +1070,9 @@ class FusedAdamEngine:
         self._ts_keep = None
         self.twoshot = None
         self.ready = False
+        self.closed = True
+        self.graph = None
+        self._gkey = None
 
     def _ts_pack(self, c: int) -> bytes:
         """Chunk c's two-shot exchange (reduce-scatter -> Adam -> all-gather; bounded fits:
@@ -1360,6 +1485,7 @@ class FusedAdamEngine:
         finally:
             self._capturing = False
             self.pending = pend
+        self.stats["captures"] += 1
         if k == 1:
             self.graph = g
         else:
@@ -1463,7 +1589,10 @@ class FusedAdamEngine:
         self.check("trajectory", collective=True)
         if self.traj_loc is None:
             if self.history.mode == "full":
-                return self._traj_to_user(self.history.result())
+                out = self._traj_to_user(self.history.result())
+                if out.untyped_storage().data_ptr() == self.history.buf.untyped_storage().data_ptr():
+                    out = out.clone()  # the buffer is the engine's: a later run rewrites it
+                return out
             return self.to_user(self.history.result())
         if self.owner:
             rows = self.step_host + 1
@@ -1693,6 +1822,14 @@ class FusedAdamEngine:
             return pos
 
         cur = self._local_order()
+        if not torch.equal(saved, cur) and self.zero and not self.owner:
+            # ZeRO slices are cut from the internal order: a different lanes layout gives
+            # every rank different parameters in its slices
+            raise ValueError(
+                "this ZeRO checkpoint was written with a different lanes layout (parameter "
+                "order) than this engine's -- e.g. resumed from another starting point whose "
+                "narrow populations group the lanes differently; resume with the run's own "
+                "guess, with zero=False, or with MULTIGRAD_LANE_CLASSES=0 on both runs")
         if not torch.equal(saved, cur):
             idx = positions(saved)[cur]  # position of each current local element when saved
             n = cur.numel()
@@ -1853,10 +1990,23 @@ class _EngineObjective:
         self.e.check("L-BFGS evaluation")
         return f, g
 
+    def check(self, where: str = "L-BFGS") -> None:
+        """Collective: raise :class:`~multigrad_amd.parallel.xgmi.CollectiveTimeout` on every
+        rank if any peer-memory exchange of the engine's evaluations timed out (the two-shot
+        reduce-scatter / all-gather of the ZeRO evaluations, the one-shot sumstats) -- their
+        results were NaN-poisoned.  :meth:`device_call` does not sync, so the optimizers call
+        this at the end of a run, next to their reducer's check."""
+        self.e.check(where, collective=True)
+
     def device_call(self, x: torch.Tensor):
         """``(loss, grad)`` with the loss left on the device (1-element tensor), so the
         optimizer can fetch it together with its own reductions in one copy."""
         e, md = self.e, self.e.model
+        self._nev = getattr(self, "_nev", 0) + 1
+        if self._fault_now():
+            # test hook: this rank skips the gradient exchange of one evaluation, so its
+            # peers' bounded waits time out (the engine's error word, NaN-poisoned slices)
+            return e.loss, e.g_loc if (e.zero and not e.owner) else e.grad
         self._load(x)
         e._forward_loss()
         if e.owner:
@@ -1888,6 +2038,15 @@ class _EngineObjective:
                 e.comm.all_reduce(e.grad)
             g = e.grad
         return e.loss, g
+
+    def _fault_now(self) -> bool:
+        """``MULTIGRAD_LBFGS_FAULT=<rank>:<evaluation>`` (tests): that rank skips the whole
+        evaluation number ``evaluation`` (1-based) -- every exchange in it."""
+        spec = os.environ.get("MULTIGRAD_LBFGS_FAULT")
+        if not spec or self.e.size == 1:
+            return False
+        r, _, k = spec.partition(":")
+        return int(r) == self.e.rank and int(k or 1) == self._nev
 
     def full(self, x: torch.Tensor) -> torch.Tensor:
         """The full parameter vector (model order) for the optimizer's vector x."""

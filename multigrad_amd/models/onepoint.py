@@ -139,7 +139,8 @@ class _OptimizerFrontEnds:
                     return eng.run_adam(guess, nsteps=nsteps, param_bounds=param_bounds,
                                         learning_rate=learning_rate, **kw)
                 finally:
-                    eng.close()
+                    if not getattr(eng, "cached", False):  # a model's cached engine stays up
+                        eng.close()
         # any other model or group on a GPU: one captured step replayed per iteration
         # (engine/generic.py), per-step or constant keys included
         graph_kw = {k: kw[k] for k in kw if k in ("history", "legacy_bounds_jacobian", "b1",
@@ -209,7 +210,8 @@ class _OptimizerFrontEnds:
                     lo, hi = obj.local_box(param_bounds)
                     return _lbfgsb.lbfgsb_minimize(obj, lo, hi, maxiter=maxsteps, m=hist, **kw)
                 finally:
-                    eng.close()
+                    if not getattr(eng, "cached", False):
+                        eng.close()
         if param_bounds is not None and mode == "project":
             return _lbfgsb.run_lbfgsb_device(self.calc_loss_and_grad_from_params, x0,
                                              maxsteps=maxsteps, param_bounds=param_bounds,

@@ -313,9 +313,36 @@ class PopulationSMFModel(OnePointModel):
     # ------------------------------------------------------------ fused-engine protocol
     # (see multigrad_amd.engine.fused): parameters are grouped in "units" of 2 (one
     # population); the engine chooses unit-aligned chunk boundaries.
-    def fused_engine(self, **kw):
+    def fused_engine(self, cache: bool = True, **kw):
+        """The model's fused Adam engine.  Cached per model and keyword set (``cache``): a
+        repeated ``run_adam`` / ``run_bfgs`` re-uses its buffers, layout, autotune verdict
+        and -- with unchanged buffers and scalars -- its captured graphs (engine/fused.py
+        ``stats``), the analogue of the jit cache the reference's benchmark warms once
+        (tests/smf_example/benchmark.py:41-46).  Replacing ``aux_data`` entries (a new
+        shard) or closing the engine drops it."""
         from ..engine.fused import FusedAdamEngine
-        return FusedAdamEngine(self, **kw)
+        if not cache:
+            return FusedAdamEngine(self, **kw)
+        comm = kw.get("comm", None)
+        key = (tuple(sorted((k, repr(v)) for k, v in kw.items())), id(self.aux_data.get("shard")),
+               id(self.comm if comm is None else comm))
+        store = self.__dict__.setdefault("_engine_cache", {})
+        eng = store.get(key)
+        if eng is None or getattr(eng, "closed", False):
+            eng = FusedAdamEngine(self, **kw)
+            eng.cached = True
+            store[key] = eng
+        return eng
+
+    def engine_chunks_current(self, unit_bounds) -> bool:
+        """Whether the shard is already cut at ``unit_bounds`` (the engine then keeps the
+        layout instead of rebuilding it, when the lane classes did not change either)."""
+        return list(getattr(self.shard, "chunk_pops", [])) == [int(u) for u in unit_bounds]
+
+    def engine_layout_epoch(self):
+        """Changes whenever the device layout is rebuilt (part of the engine's graph key)."""
+        sh = self.shard
+        return (id(sh), getattr(sh, "layout_version", 0))
 
     def engine_units(self):
         """(number of parameter units, parameters per unit)."""

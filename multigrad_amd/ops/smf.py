@@ -204,6 +204,8 @@ class PopulationShard:
         rebuild the tile schedule so that no tile straddles a chunk boundary."""
         pb = [int(b) for b in pop_bounds]
         assert pb[0] == 0 and pb[-1] == self.npop and all(a <= b for a, b in zip(pb, pb[1:]))
+        # bumped by every (re)build: engines key their captured graphs on it
+        self.layout_version = getattr(self, "layout_version", 0) + 1
         self.nchunks = len(pb) - 1
         self.chunk_pops = pb
         self.chunk_halos = [int(self.offsets[b]) for b in pb]

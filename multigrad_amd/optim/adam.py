@@ -134,12 +134,15 @@ class History:
     would be tens of GB).
     """
 
-    def __init__(self, mode, nsteps: int, first: torch.Tensor):
+    def __init__(self, mode, nsteps: int, first: torch.Tensor, buf: Optional[torch.Tensor] = None):
         self.mode = mode
         self.nsteps = int(nsteps)
         if mode == "full":
-            self.buf = torch.empty((self.nsteps + 1,) + tuple(first.shape), dtype=first.dtype,
-                                   device=first.device)
+            shape = (self.nsteps + 1,) + tuple(first.shape)
+            if buf is None or tuple(buf.shape) != shape or buf.dtype != first.dtype or \
+                    buf.device != first.device:
+                buf = torch.empty(shape, dtype=first.dtype, device=first.device)
+            self.buf = buf   # ``buf``: an engine's buffer of a previous run, re-used
             self.buf[0].copy_(first)
         else:
             self.rows = [first.detach().clone()]

@@ -102,6 +102,9 @@ def _lbfgs_minimize_impl(obj, maxiter: int = 100, m: int = 10, ftol: float = 1e7
     comm, sharded = obj.comm, obj.sharded
     n = obj.n_local
     dev = obj.device
+    if not 1 <= int(m) <= 120:
+        # 2 (m + 1) history rows go through one lincomb launch (csrc/lbfgs.hip: <= 256 rows)
+        raise ValueError(f"L-BFGS history m must be in 1..120, got {m}")
     red = DeviceReducer(comm, sharded, dev)  # collective (may connect peer memory)
     x = obj.x0().contiguous()
     f, g = obj(x)
@@ -255,6 +258,8 @@ def _lbfgs_minimize_impl(obj, maxiter: int = 100, m: int = 10, ftol: float = 1e7
                 break
     host_calls = (getattr(comm, "host_collectives", 0) - host0) if comm is not None else 0
     red.check("L-BFGS")
+    if getattr(obj, "check", None) is not None:
+        obj.check("L-BFGS")  # the objective's own exchanges (engine: ZeRO two-shot, one-shot)
     xf = obj.full(x)
     if getattr(obj, "finalize", None) is not None:
         xf = obj.finalize(x)

@@ -192,3 +192,33 @@ def test_engine_rejects_unknown_options():
     m, data = _model()
     with pytest.raises(TypeError):
         FusedAdamEngine(m).run_adam(data["guess"], nsteps=1, not_an_option=3)
+
+
+def _zero_layout_resume(rank, size, tmp):
+    comm = mg.get_world_comm()
+    data = make_population_data(num_params=NP, num_halos=NH, seed=11, comm=comm, device="cpu",
+                                layout="lanes")
+    m = PopulationSMFModel(aux_data=data, comm=comm)
+    m.set_target_from_truth()
+    ck = f"{tmp}/zero.ckpt"
+    e1 = FusedAdamEngine(m, zero=True, chunks=2)
+    e1.setup(data["guess"], 4, None, 2e-3)
+    e1.step()
+    e1.save_checkpoint(ck)
+    # another starting point: a third of the populations start narrow (bin width > 0.5
+    # sigma), so the lanes are grouped differently and the internal order changes
+    g2 = data["guess"].clone()
+    g2[1::6] = -1.4
+    e2 = FusedAdamEngine(m, zero=True, chunks=2)
+    try:
+        e2.run_adam(g2, nsteps=4, learning_rate=2e-3, resume_from=ck)
+    except ValueError as exc:
+        return "refused" if "different lanes layout" in str(exc) else str(exc)
+    return "loaded"
+
+
+def test_zero_checkpoint_with_another_lanes_layout_is_refused(tmp_path):
+    """a ZeRO checkpoint loaded into an engine whose lanes layout differs is
+    refused with a clear error (its slices would hold other parameters)."""
+    res = run_distributed(_zero_layout_resume, 2, str(tmp_path))
+    assert res == ["refused", "refused"], res

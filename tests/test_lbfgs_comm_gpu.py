@@ -164,3 +164,23 @@ def test_device_lbfgsb_two_ranks_one_gpu_no_host_collectives():
         assert f == pytest.approx(f1, rel=2e-4, abs=1e-9)
         np.testing.assert_allclose(x, x1, rtol=2e-4, atol=2e-5)
     np.testing.assert_array_equal(res[1][0], res[0][0])
+
+
+def _lbfgs_fault(rank, size):
+    import os
+    os.environ["MULTIGRAD_ONESHOT_TIMEOUT"] = "1"
+    os.environ["MULTIGRAD_LBFGS_FAULT"] = "1:3"   # rank 1 skips the 3rd evaluation
+    from multigrad_amd.parallel.xgmi import CollectiveTimeout
+    try:
+        _lbfgs(rank, size, "hashed", iters=6)
+    except CollectiveTimeout as exc:
+        return "raised", str(exc)[:200]
+    return "returned", ""
+
+
+def test_device_lbfgs_zero_exchange_timeout_raises_on_every_rank():
+    """A peer that skips the ZeRO evaluation's two-shot exchanges makes the others' bounded
+    waits time out: the run must raise CollectiveTimeout on every rank (checked at the end of
+    the optimizer), not return a NaN iterate with an ordinary status."""
+    res = run_distributed(_lbfgs_fault, 2, timeout=600)
+    assert [r[0] for r in res] == ["raised", "raised"], res

@@ -44,8 +44,8 @@ def assert_close_bins(S, S64, rtol, atol, where):
 @pytest.mark.parametrize("which", ["test", "docs"])
 def test_fused_evaluation_matches_fp64_oracle_across_sigma(schedule, which, monkeypatch):
     """Loss, gradient and sumstats of one fused evaluation against fp64 autograd for sigma
-    from 0.15 to 0.6 (bin width 0.1: h = 0.67 .. 0.17 -- both the per-edge fallback above
-    h = 0.5 and the Euler-Maclaurin path below it)."""
+    from 0.11 to 0.6 (bin width 0.1: h = 0.91 .. 0.17 -- both the per-edge fallback above
+    h = 0.7 and the four-term Euler-Maclaurin path below it, including h = 0.67 and 0.5)."""
     monkeypatch.setenv("MULTIGRAD_SMF2_SCHEDULE", schedule)
     import multigrad_amd.parallel.comm as C
     from multigrad_amd.models.smf import DocsSMFModel, MySMFModel, make_docs_data, make_test_data
@@ -53,10 +53,10 @@ def test_fused_evaluation_matches_fp64_oracle_across_sigma(schedule, which, monk
     n = 30_000 if schedule == "loop" else 300_000
     if which == "test":
         model = MySMFModel(aux_data=make_test_data(n), device=DEV)
-        pts = [(-2.0, s) for s in (0.15, 0.18, 0.2, 0.25, 0.35, 0.5, 0.6)] + [(-1.7, 0.3)]
+        pts = [(-2.0, s) for s in (0.11, 0.13, 0.15, 0.18, 0.2, 0.25, 0.35, 0.5, 0.6)] + [(-1.7, 0.3)]
     else:
         model = DocsSMFModel(aux_data=make_docs_data(n), device=DEV)
-        pts = [(-2.0, float(np.log10(s))) for s in (0.15, 0.19, 0.21, 0.3, 0.45, 0.6)]
+        pts = [(-2.0, float(np.log10(s))) for s in (0.11, 0.14, 0.15, 0.19, 0.21, 0.3, 0.45, 0.6)]
     eng = model.fused_step_engine()
     assert eng is not None and eng.schedule == schedule
     ev = eng.evaluator()
@@ -69,8 +69,15 @@ def test_fused_evaluation_matches_fp64_oracle_across_sigma(schedule, which, monk
         _, bins = model._setup()
         atol = 4e-7 * n * np.asarray(bins.scale)
         assert_close_bins(S, S64, 2e-5, atol, p)
-        assert float(loss) == pytest.approx(l64, rel=2e-3, abs=5e-8), p
-        _, gk, _ = _oracle(model, p, S_at=S)   # the VJP at the kernel's own sumstats
+        # loss and VJP at the kernel's own sumstats: bins whose mass is a far Gaussian tail
+        # (S ~ the docs model's eps = 1e-10 at sigma = 0.15) carry the absolute error of
+        # the float32 contract -- the reference's 0.5 (1 + erf) returns exactly 0 there --
+        # which a log-MSE magnifies without bound, so the loss is checked for the epilogue's
+        # arithmetic and the sumstats above for the forward's contract
+        lk, gk, _ = _oracle(model, p, S_at=S)   # the VJP at the kernel's own sumstats
+        assert float(loss) == pytest.approx(lk, rel=1e-4, abs=1e-8), p
+        if (S64 > 1e3 * (model._loss_eps + 1e-30)).all() and (S64 > 1e-7 * S64.max()).all():
+            assert float(loss) == pytest.approx(l64, rel=2e-3, abs=5e-8), p
         np.testing.assert_allclose(grad.cpu().double().numpy(), gk, rtol=2e-4,
                                    atol=1e-6 * np.abs(gk).max(), err_msg=str(p))
 

@@ -3,7 +3,7 @@
 set -o pipefail
 O=gpurun_out/r6_smf2b
 mkdir -p $O
-timeout -k 10 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_smf2_gpu.py \
+timeout -k 10 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_smf2_gpu.py tests/test_lbfgs_comm_gpu.py \
   > $O/pytest.log 2>&1 || { tail -60 $O/pytest.log; exit 1; }
 tail -2 $O/pytest.log
 for rep in 1 2; do
