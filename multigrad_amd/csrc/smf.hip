@@ -3286,9 +3286,15 @@ __device__ __forceinline__ void smf2_em_staged(const float* __restrict__ x, int6
   }
 }
 
+constexpr int kS2StepThreads = 512;   // threads of the one-workgroup step kernel
+#ifndef MG_S2_MINWAVES
+#define MG_S2_MINWAVES 5   // resident waves per SIMD the staged forward is register-capped for
+#endif
+constexpr int kS2Unroll = 8;          // slab rows per thread in flight
+
 // Grid forward of one step: slab row per workgroup (R floats).
 template <int NB, bool LOGSIG>
-__global__ __launch_bounds__(kThreads) void smf2_fwd_kernel(const float* __restrict__ x, int64_t n,
+__global__ __launch_bounds__(kThreads, MG_S2_MINWAVES) void smf2_fwd_kernel(const float* __restrict__ x, int64_t n,
                                                             const float* __restrict__ theta,
                                                             SmfBins b, float* __restrict__ slab) {
   using EP = EdgePairs<NB>;
@@ -3324,26 +3330,42 @@ __global__ __launch_bounds__(kThreads) void smf2_fwd_kernel(const float* __restr
 // update.  mode 0: the whole step; 1: sums only, to P.vals (the caller all-reduces them on
 // RCCL / gloo); 2: the step from the global sums in P.vals.
 template <int NB, bool LOGSIG>
-__global__ __launch_bounds__(kEpiThreads) void smf2_step_kernel(const float* __restrict__ slab,
-                                                                int nrows, Smf2Step P, SmfBins b,
-                                                                int mode) {
+__global__ __launch_bounds__(kS2StepThreads) void smf2_step_kernel(const float* __restrict__ slab,
+                                                                   int nrows, Smf2Step P, SmfBins b,
+                                                                   int mode) {
   constexpr int R = S2<NB>::R;
+  constexpr int G = kS2StepThreads / R;   // row groups of the coalesced slab sum
   __shared__ float vals[R];
-  __shared__ double scratch[R * (kEpiThreads / kWave)];
+  __shared__ double part[G * R];
   if (mode == 2) {
     if (threadIdx.x < R) vals[threadIdx.x] = P.vals[threadIdx.x];
     __syncthreads();
   } else {
-    double v[R];
+    // The slab is read as one flat array: thread t sums column t % R of rows t / R, t / R + G,
+    // ... (consecutive threads read consecutive floats, kS2Unroll rows in flight), then
+    // thread c < R adds its column's G partials -- a fixed order, the same bits every step.
+    // (Row-per-thread sums issued one dependent round trip per row: 17 us at 1024 rows.)
+    const int t = threadIdx.x;
+    if (t < G * R) {
+      const int c = t % R;
+      double acc = 0.0;
+      int r = t / R;
+      for (; r + (kS2Unroll - 1) * G < nrows; r += kS2Unroll * G) {
+        float x[kS2Unroll];
 #pragma unroll
-    for (int k = 0; k < R; ++k) v[k] = 0.0;
-    for (int r = threadIdx.x; r < nrows; r += kEpiThreads) {
+        for (int u = 0; u < kS2Unroll; ++u) x[u] = slab[(int64_t)(r + u * G) * R + c];
 #pragma unroll
-      for (int k = 0; k < R; ++k) v[k] += (double)slab[(int64_t)r * R + k];
+        for (int u = 0; u < kS2Unroll; ++u) acc += (double)x[u];
+      }
+      for (; r < nrows; r += G) acc += (double)slab[(int64_t)r * R + c];
+      part[t] = acc;
     }
-    __shared__ double dsum[R];
-    block_sum_par<R>(v, scratch, dsum);
-    for (int k = threadIdx.x; k < R; k += kEpiThreads) vals[k] = (float)dsum[k];
+    __syncthreads();
+    if (t < R) {
+      double s = part[t];
+      for (int g = 1; g < G; ++g) s += part[g * R + t];
+      vals[t] = (float)s;
+    }
     __syncthreads();
     if (mode == 1) {
       if (threadIdx.x < R) P.vals[threadIdx.x] = vals[threadIdx.x];
@@ -3517,7 +3539,7 @@ void smf2_step(torch::Tensor slab, int64_t nrows, std::vector<double> edges, std
     TORCH_CHECK(mode == 2 || (nrows >= 1 && slab.numel() >= nrows * R), "smf2: slab too small");
     Smf2Step P = make_s2(state, scalars, mode == 0 ? peers : std::vector<int64_t>(), rank, seq, err, nb, R);
     with_bool(log_sigma, [&](auto LS) {
-      hipLaunchKernelGGL((smf2_step_kernel<NB, decltype(LS)::value>), dim3(1), dim3(kEpiThreads), 0,
+      hipLaunchKernelGGL((smf2_step_kernel<NB, decltype(LS)::value>), dim3(1), dim3(kS2StepThreads), 0,
                          stream, slab.data_ptr<float>(), (int)nrows, P, b, (int)mode);
     });
   });

@@ -808,6 +808,16 @@ class FusedAdamEngine:
     def _autotune(self, cands, warm: int = 2, min_window_s: float = 0.008, **kw):
         key = self._tune_key(cands)
         hit = self._tune_cache.get(key)
+        if hit is not None and hit.get("budget_skipped"):
+            # a short run kept the default schedule before: again, unless this run's budget
+            # (from the probe step time measured then) now affords the windows
+            est = hit["step_ms_probe"] * 1e-3
+            budget = float(os.environ.get("MULTIGRAD_TUNE_BUDGET", "0.1")) * est * max(1, self.nsteps)
+            rounds_b = max(1, int(os.environ.get("MULTIGRAD_AUTOTUNE_ROUNDS", "2")))
+            extra = warm + (self.graph_steps if any(c.get("use_graph") for c in cands) else 0)
+            if _autotune_mode() == "on" or \
+                    int(budget / max(est, 1e-9) / (len(cands) * rounds_b)) - extra >= 8:
+                hit = None
         if hit is not None:
             # this engine timed these candidates before (a repeated run_* call): no trial
             # steps, the verdict is applied as it is
@@ -815,7 +825,9 @@ class FusedAdamEngine:
             for k, v in hit["chosen"].items():
                 if getattr(self, k, None) != v:
                     setattr(self, k, v)
-                    changed = True
+                    # use_graph / graph_steps choose whether (and which) graphs replay; the
+                    # graphs themselves stay valid (their buffers are in the graph key)
+                    changed = changed or k not in ("use_graph", "graph_steps")
             if changed:
                 self.graph = None
             self.tuning = dict(hit, cached=True)
@@ -826,7 +838,7 @@ class FusedAdamEngine:
             self._autotune_impl(cands, warm, min_window_s, **kw)
         finally:
             trace(f"engine: autotune done {getattr(self, 'tuning', None)}")
-        if self.tuning is not None and not self.tuning.get("budget_skipped"):
+        if self.tuning is not None:
             self._tune_cache[key] = {k: v for k, v in self.tuning.items() if k != "cached"}
 
     def _autotune_impl(self, cands, warm: int = 2, min_window_s: float = 0.008,

@@ -217,9 +217,10 @@ class Smf2Engine:
                         float(self._cap), lo[0], lo[1], hi[0], hi[1], float(timeout)]
         self.step_host = 0
         self.stats["setups"] += 1
-        if self.schedule == "grid" and self.use_graph and code != 2 and \
-                nsteps >= self.graph_steps > 1:
-            self._graph(self.graph_steps)  # captured once per schedule, then cached
+        if self.schedule == "grid" and self.use_graph and code != 2 and self.graph_steps > 1:
+            # captured once per schedule (even by a 1-step warm-up call: the "compile" step
+            # of the reference's benchmark), then cached
+            self._graph(self.graph_steps)
         return self
 
     # ------------------------------------------------------------------ launches

@@ -47,6 +47,9 @@ def test_short_first_run_keeps_the_tuning_within_budget():
     eng = m.fused_engine()
     assert eng.tuning.get("budget_skipped"), eng.tuning
     assert eng.stats["trial_steps"] <= 4 + 10 + 1, eng.stats
+    n = eng.stats["trial_steps"]
+    m.run_adam(data["guess"], nsteps=100, learning_rate=1e-3)   # the same short run again
+    assert eng.tuning.get("cached") and eng.stats["trial_steps"] == n, eng.stats
 
 
 def test_new_data_rebuilds_the_cached_engine():
