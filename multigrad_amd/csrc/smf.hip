@@ -925,12 +925,35 @@ __device__ __forceinline__ EmLane em_lane(float inv, float delta) {
   return L;
 }
 
+// Two-term Euler-Maclaurin (B_2, B_4 only: c1 = h^2/12 + 3h^4/720, c3 = -h^4/720): its
+// remainder, the B_6 term, is at most 1.26e-7 of one halo's unit mass per bin at
+// h = 0.35 (8.3e-8 at 0.33, 1.2e-8 at 0.25; maximum over the halo position, checked in
+// float64 against the exact Gaussian integral), inside the absolute contract of the
+// per-edge tails (1.6e-7).  A lane group whose widths are all <= kEmH2 skips the z^5 term:
+// one packed FMA per edge pair per halo less (~6 of ~78 VALU per halo).  The headline
+// populations sit at h = 0.2 .. 0.32.
+constexpr float kEmH2 = 0.35f;
+
+__device__ __forceinline__ EmLane em_lane2(float inv, float delta) {
+  constexpr float ik = 1.0f / kWScale;
+  EmLane L;
+  L.inv = inv;
+  const float dw = delta * inv;
+  L.dw4 = -4.0f * dw;
+  const float h = dw * ik;
+  const float h2 = h * h, h4 = h2 * h2;
+  L.a1 = (h2 * (1.0f / 12.0f) + h4 * (3.0f / 720.0f)) * ik;
+  L.a3 = -(h4 * (1.0f / 720.0f)) * (ik * ik * ik);
+  L.a5 = 0.0f;
+  return L;
+}
+
 // One halo (nm = -(x + a) inv): F, Wa, E accumulate the UNSCALED sums of edge pairs (the
 // pair layout of EdgePairs; an odd last edge in the .x half of the extra pair).  The lane
 // constants come as scalars, not as the EmLane struct: splats of adjacent struct fields were
 // widened into 8-byte loads that kept (a1, a3, a5) in private memory, a scratch store and two
 // scratch loads at every group start of the headline kernel.
-template <int NB, bool RESID, bool A7 = false>
+template <int NB, bool RESID, bool A7 = false, bool A5 = true>
 __device__ __forceinline__ void em_halo(float nm, float inv, float dw4, float a1, float a3,
                                         float a5, const SmfBins& b,
                                         v2f (&F)[EdgePairs<NB>::NV], v2f (&Wa)[EdgePairs<NB>::NV],
@@ -959,10 +982,13 @@ __device__ __forceinline__ void em_halo(float nm, float inv, float dw4, float a1
     if constexpr (A7) {
       t = w2 * a7 + a5;
       t = t * w2 + a3;
-    } else {
+      t = t * w2 + a1;
+    } else if constexpr (A5) {
       t = w2 * a5 + a3;
+      t = t * w2 + a1;
+    } else {
+      t = w2 * a3 + a1;
     }
-    t = t * w2 + a1;
     E[i] = pw * t + E[i];
   };
   const v2f ws = wpair(M);
@@ -986,7 +1012,7 @@ __device__ __forceinline__ void em_halo(float nm, float inv, float dw4, float a1
     if constexpr (RESID) Wa[EP::NP].x += pw;
     const float w2 = wz * wz;
     const float t = A7 ? fmaf(fmaf(fmaf(w2, a7, a5), w2, a3), w2, a1)
-                       : fmaf(fmaf(w2, a5, a3), w2, a1);
+                       : (A5 ? fmaf(fmaf(w2, a5, a3), w2, a1) : fmaf(w2, a3, a1));
     E[EP::NP].x = fmaf(pw, t, E[EP::NP].x);
   }
   if constexpr (M > 0) {
@@ -1002,12 +1028,12 @@ __device__ __forceinline__ void em_halo(float nm, float inv, float dw4, float a1
 
 // Keep the scheduler from interleaving consecutive halos (their
 // temporaries would double the register footprint of the pipelined-update kernel)
-template <int NB, bool RESID>
+template <int NB, bool RESID, bool A5 = true>
 __device__ __forceinline__ void lane_halo_em(float x, const EmLane& L, float nma,
                                              const SmfBins& b, v2f (&F)[EdgePairs<NB>::NV],
                                              v2f (&Wa)[EdgePairs<NB>::NV],
                                              v2f (&E)[EdgePairs<NB>::NV]) {
-  em_halo<NB, RESID>(fmaf(x, -L.inv, nma), L.inv, L.dw4, L.a1, L.a3, L.a5, b, F, Wa, E);
+  em_halo<NB, RESID, false, A5>(fmaf(x, -L.inv, nma), L.inv, L.dw4, L.a1, L.a3, L.a5, b, F, Wa, E);
   __builtin_amdgcn_sched_barrier(0);
 }
 
@@ -1380,6 +1406,11 @@ __global__ __launch_bounds__(kThreads, XS == 2 ? 6 : MG_VJP_REC_MINWAVES) void s
 // workgroup of the lanes forward (headline 0.4352-0.4357 vs 0.4352-0.4364 ms/step, owner
 // proxy 0.0626-0.0628 vs 0.0618-0.0619: not faster than its own one-workgroup launch).
 constexpr int kLanesMainMode = 3;
+
+// Two-term Euler-Maclaurin groups (kEmH2) in the lanes forward: 1 = on (default), 0 = off
+#ifndef MG_EM2
+#define MG_EM2 1
+#endif
 
 // Minimum resident waves per SIMD of the lanes forward: the edge-pair path needs up to 128
 // VGPRs (4 waves/SIMD) to avoid spills; at 5 or 6 waves it spills.
@@ -1780,28 +1811,36 @@ __global__ __launch_bounds__(kThreads, MG_LANES_MINWAVES) void smf_fwd_lanes_ker
     }
     // Euler-Maclaurin path (see em_halo) when every occupied lane's bin width is inside
     // kEmHMax; the ballot makes the choice wave-uniform
-    bool em = false;
+    bool em = false, em2 = false;
     if constexpr (kEm) {
       const float inv = -ninv;
-      const bool bad = c_cur >= 0 && !(bins.delta * inv * (1.0f / kWScale) <= kEmHMax);
+      const float h = bins.delta * inv * (1.0f / kWScale);
+      const bool bad = c_cur >= 0 && !(h <= kEmHMax);
       em = bins.delta > 0.0f && __builtin_amdgcn_ballot_w64(bad) == 0;
+#if MG_EM2
+      em2 = em && __builtin_amdgcn_ballot_w64(c_cur >= 0 && !(h <= kEmH2)) == 0;
+#endif
     }
     if constexpr (kEm) if (em) {
-      const EmLane eml = em_lane(-ninv, bins.delta);
+      const EmLane eml = em2 ? em_lane2(-ninv, bins.delta) : em_lane(-ninv, bins.delta);
       v2f Ep[EP::NV];
 #pragma unroll
       for (int e = 0; e < EP::NV; ++e) Ep[e] = (v2f)(0.0f);
-      for (int j = 0; j < len; j += kLanesUnroll) {
-        float xc[kLanesUnroll];
+      auto em_loop = [&](auto a5c) {
+        for (int j = 0; j < len; j += kLanesUnroll) {
+          float xc[kLanesUnroll];
 #pragma unroll
-        for (int u = 0; u < kLanesUnroll; ++u) {
-          xc[u] = lane_use(xn[u], j + u, len);
-          xn[u] = lane_load(xp, j + kLanesUnroll + u, len);
+          for (int u = 0; u < kLanesUnroll; ++u) {
+            xc[u] = lane_use(xn[u], j + u, len);
+            xn[u] = lane_load(xp, j + kLanesUnroll + u, len);
+          }
+#pragma unroll
+          for (int u = 0; u < kLanesUnroll; ++u)
+            lane_halo_em<NB, RESID, decltype(a5c)::value>(xc[u], eml, -mua, bins, Gp, Wp, Ep);
         }
-#pragma unroll
-        for (int u = 0; u < kLanesUnroll; ++u)
-          lane_halo_em<NB, RESID>(xc[u], eml, -mua, bins, Gp, Wp, Ep);
-      }
+      };
+      if (em2) em_loop(std::false_type{});   // two-term EM (the group's h <= kEmH2)
+      else em_loop(std::true_type{});
       em_group_end<NB>(eml, Gp, Wp, Ep, accp);
     }
     // the next kLanesUnroll loads are in flight while the current halos are computed;

@@ -7,6 +7,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 os.environ.setdefault("MULTIGRAD_PROGRESS", "0")
+# the engine tests were written against the full setup autotune (every candidate timed,
+# however short the run); the library default budgets it to 10 % of the run, which
+# tests/test_engine_cache_gpu.py covers explicitly
+os.environ.setdefault("MULTIGRAD_AUTOTUNE", "on")
 
 
 def pytest_configure(config):

@@ -10,6 +10,11 @@ pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda", 0)
 
 
+@pytest.fixture(autouse=True)
+def _budgeted_autotune(monkeypatch):
+    monkeypatch.setenv("MULTIGRAD_AUTOTUNE", "auto")   # the library default
+
+
 def _model(npar=20_000, nhalo=400_000):
     import multigrad_amd.parallel.comm as C
     from multigrad_amd.models.population import PopulationSMFModel, make_population_data
