@@ -15,6 +15,7 @@ import numpy as np
 import torch
 
 from ._ext import ext
+from ..utils.trace import trace
 
 __all__ = ["SmfBins", "PopulationShard", "smf_sumstats", "smf_sumstats_reference",
            "logmse_loss", "normal_cdf", "TILE_HALOS", "TILE_POPS"]
@@ -170,6 +171,7 @@ class PopulationShard:
             self.pop = None
         else:
             pop = torch.as_tensor(pop).reshape(-1)
+            trace(f"shard: sort {pop.numel()} halos into {self.npop} populations")
             if pop.device.type == "cuda":
                 # device radix sort + histogram; only the J counts come back to the host
                 spop, order, counts = stable_population_sort(pop.to(torch.int32), self.npop)
@@ -190,9 +192,11 @@ class PopulationShard:
         self.order_counts = None
         self.lane_class = None  # optional per-population class that groups lanes first
         if self.layout == "lanes" and lane_order == "global" and comm is not None and comm.size > 1:
+            trace("shard: all-reduce of the population counts (global lane order)")
             oc = counts.clone().to(torch.int64)
             comm.all_reduce(oc)
             self.order_counts = oc
+        trace("shard: counts ready")
         self.offsets = torch.zeros(self.npop + 1, dtype=torch.int64)
         self.offsets[1:] = torch.cumsum(counts, 0)
         self._tile_halos, self._tile_pops = tile_halos, tile_pops
@@ -304,6 +308,7 @@ class PopulationShard:
                 out = build_lanes_py(self.counts, pb[1:-1], self._lane_window, self._lane_lmax, key)
         (slot_pop, slot_src, slot_len, slot_part, group_base, group_len, chunk_groups, giant,
          chunk_giant, fwd_order, slot_pidx, perm) = out
+        trace(f"shard: lanes schedule built ({int(group_len.numel())} groups)")
         dev = self.device
         self.nslots = int(slot_pop.numel())
         self.ngroups = int(group_len.numel())
@@ -340,6 +345,7 @@ class PopulationShard:
         self.resid = None
         self.resid_epoch += 1
         self._pe_share = None
+        trace("shard: lanes packed")
 
     def fwd_schedule(self, chunk: Optional[int], nblocks: int):
         """Work distribution of the lanes forward over ``chunk`` with ``nblocks``
@@ -348,21 +354,24 @@ class PopulationShard:
         ``MULTIGRAD_LPT``: ``static`` -- per-wave LPT lists built on the host
         (runtime.cpp:lpt_waves); ``dynamic`` -- 256 device work queues drawn by atomic
         tickets (waves that the oldest-first issue arbitration favours take more groups);
-        ``0`` -- grid-stride over the longest-first order; ``auto`` (default) -- dynamic
-        when every wave gets >= 8 groups, static otherwise.  The static lists run with
-        issue-priority feedback (``MG_FWD_PRIO`` in smf.hip: a wave's priority falls as
-        its list drains), which removes most of the oldest-wave-first tail.  Measured on
-        one MI355X (profiles/fwd_prio_ab.md): kernel alone 543 us static+priority vs
-        551 dynamic at 1.34e8 halos, but the pipelined bench step 0.641 vs 0.636 ms, so
-        dynamic stays at that size; at 1/8 (the 8-GPU owner shard) 0.0993 vs 0.1045 ms
-        per step (0.1086 before the priority feedback).
+        ``0`` -- grid-stride over the longest-first order; ``auto`` (default) -- static.
+        The static lists run with issue-priority feedback (``MG_FWD_PRIO`` in smf.hip: a
+        wave's priority falls as its list drains), which removes most of the
+        oldest-wave-first tail.  Until round 5 ``auto`` took the dynamic queues when every
+        wave got >= 8 groups (the headline); round 6 measured static faster at every size
+        of the pipelined step, same box, 3 alternating pairs (profiles/r6_owner_tail/):
+        headline 0.4335-0.4341 vs 0.4352-0.4354 ms, 1/4 owner proxy 0.1137-0.1139 vs
+        0.1181-0.1185, 1/8 0.0628-0.0630 vs 0.0713-0.0718.  Static lists also make the
+        forward's bin sums run-to-run reproducible: a wave accumulates its groups in list
+        order, while the dynamic draws change which wave sums which group (one of the
+        three dynamic 1/4 runs ended at a different last-digit loss).
         """
         mode = os.environ.get("MULTIGRAD_LPT", "auto")
         if mode == "0":
             return None, None, None
         g0, g1 = self.group_range(chunk)
         nwaves = int(nblocks) * (256 // 64)
-        if mode == "dynamic" or (mode == "auto" and g1 - g0 >= 8 * nwaves):
+        if mode == "dynamic":
             if getattr(self, "_queues", None) is None:
                 if self.device.type == "cuda" and torch.cuda.is_current_stream_capturing():
                     return None, None, None

@@ -4,7 +4,7 @@
 set -o pipefail
 O=gpurun_out/r6_n8
 mkdir -p $O
-MULTIGRAD_TRACE=1 NPROC=8 PLACEMENT=repartition timeout -k 10 400 bash tools/bench_2rank.sh --steps 20 --warmup 5 --no-count-launches \
+GPU_MAX_HW_QUEUES=${HWQ:-4} MULTIGRAD_TRACE=1 NPROC=8 PLACEMENT=repartition timeout -k 10 400 bash tools/bench_2rank.sh --steps 20 --warmup 5 --no-count-launches \
   > $O/bench_n8.json 2> $O/bench_n8.err; rc=$?
 grep -v "amdgpu.ids\|socket.cpp" $O/bench_n8.err | tail -60
 echo "rc=$rc"
