@@ -324,13 +324,20 @@ class PopulationSMFModel(OnePointModel):
         if not cache:
             return FusedAdamEngine(self, **kw)
         comm = kw.get("comm", None)
-        key = (tuple(sorted((k, repr(v)) for k, v in kw.items())), id(self.aux_data.get("shard")),
+        sid = id(self.aux_data.get("shard"))
+        key = (tuple(sorted((k, repr(v)) for k, v in kw.items())), sid,
                id(self.comm if comm is None else comm))
         store = self.__dict__.setdefault("_engine_cache", {})
+        # engines of a replaced shard are dropped (each holds its shard, its layout and
+        # O(params) device buffers; a cached engine keeps its shard alive, so a shard id in
+        # the key cannot be reused by new data while the entry exists)
+        for k in [k for k in store if k[1] != sid]:
+            del store[k]
         eng = store.get(key)
         if eng is None or getattr(eng, "closed", False):
             eng = FusedAdamEngine(self, **kw)
             eng.cached = True
+            eng._cache_shard = self.aux_data.get("shard")  # pins the id in the key
             store[key] = eng
         return eng
 
@@ -421,7 +428,16 @@ class PopulationSMFModel(OnePointModel):
         if self.comm is None or self.comm.size == 1 or d.get("placement") == "owner" \
                 or self.shard.pop is None:
             return None
+        old = id(d.get("shard"))
         repartition_by_owner(d, self.comm)
+        # the engines cached for the data-parallel shard now run on the owner shard: re-key
+        # them, so the next run_* call finds the same engine (fused_engine drops entries of
+        # any other shard)
+        store = self.__dict__.get("_engine_cache", {})
+        for k in [k for k in store if k[1] == old]:
+            eng = store.pop(k)
+            eng._cache_shard = d["shard"]
+            store[(k[0], id(d["shard"]), k[2])] = eng
         return d["repartition"]
 
     def engine_owner_units(self):

@@ -146,3 +146,40 @@ def test_engine_repartition_can_be_turned_off():
     os.environ.pop("MULTIGRAD_REPARTITION", None)
     res = run_distributed(_engine_off, 2, timeout=300)
     assert all((not o) and z and p == "hashed" for o, z, p in res)
+
+
+def _cached_after_repartition(rank, size):
+    os.environ.pop("MULTIGRAD_REPARTITION", None)
+    comm = mg.get_world_comm()
+    data = make_population_data(num_params=NP, num_halos=NH, seed=11, comm=comm, device="cpu")
+    m = PopulationSMFModel(aux_data=data, comm=comm)
+    m.set_target_from_truth()
+    e1 = m.fused_engine()
+    e1.run_adam(data["guess"], nsteps=2, learning_rate=2e-3)
+    hashed_id = id(e1._cache_shard)
+    e2 = m.fused_engine()
+    e2.run_adam(data["guess"], nsteps=2, learning_rate=2e-3)
+    return (e1 is e2, data["placement"], len(m._engine_cache), e2.stats["setups"],
+            id(data["shard"]) == hashed_id)
+
+
+def test_cached_engine_survives_its_repartition():
+    """The engine re-partitions the model's data at its first setup; the model's engine
+    cache is re-keyed to the owner shard, so the next run_* call re-uses the same engine
+    (one cache entry, a second setup of the same object)."""
+    res = run_distributed(_cached_after_repartition, 2, timeout=300)
+    for same, placement, entries, setups, pinned in res:
+        assert same and placement == "owner" and entries == 1 and setups == 2 and pinned
+
+
+def test_replaced_shard_drops_the_cached_engine():
+    C.set_world_comm(None)
+    data = make_population_data(num_params=NP, num_halos=NH, seed=11, device="cpu")
+    m = PopulationSMFModel(aux_data=data)
+    m.set_target_from_truth()
+    e1 = m.fused_engine()
+    m.aux_data["shard"] = make_population_data(num_params=NP, num_halos=NH, seed=12,
+                                               device="cpu")["shard"]
+    e2 = m.fused_engine()
+    assert e2 is not e1 and len(m._engine_cache) == 1
+    assert m.fused_engine() is e2
