@@ -163,12 +163,17 @@ def _peer(comm, tensor, out, C, wpr: int) -> bool:
             doff.append(off)
             off += rw[q]
         recv = _words(out) if out.numel() else torch.zeros(0, dtype=torch.int32, device=out.device)
-        if off:
-            E.xgmi_a2a_pull(srcs, rw, doff, recv)
-        got = segment_checksums(recv, rw)
-        want = [info[q][1][r] for q in range(W)]
-        good = got == want
-        torch.cuda.synchronize()
+        try:  # a rank that fails here must still reach the verdict all-gather below
+            if off:
+                E.xgmi_a2a_pull(srcs, rw, doff, recv)
+            got = segment_checksums(recv, rw)
+            want = [info[q][1][r] for q in range(W)]
+            good = got == want
+            torch.cuda.synchronize()
+        except Exception as exc:  # noqa: BLE001
+            from .xgmi import _debug
+            _debug(exc)
+            good = False
     verdicts = comm.allgather(bool(good))   # also: no rank frees its region before all pulled
     if E is not None:
         for q, p in enumerate(peers):
