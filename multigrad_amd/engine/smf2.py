@@ -259,6 +259,10 @@ class Smf2Engine:
             with torch.cuda.graph(g, stream=torch.cuda.current_stream()):
                 for _ in range(k):
                     self._launch_grid_step()
+            # one graph per scalar set (learning rate, optimizer, bounds): a sweep over
+            # learning rates must not grow the cache without bound
+            while len(self._graphs) >= 8:
+                self._graphs.pop(next(iter(self._graphs)))
             self._graphs[key] = g
             self.stats["captures"] += 1
         return g
