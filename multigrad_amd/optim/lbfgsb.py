@@ -252,9 +252,9 @@ def _lbfgsb_minimize_impl(obj, lo=None, hi=None, maxiter: int = 100, m: int = 10
         else:
             r = g + th * (xcp - x)
         rF = torch.where(free, r, torch.zeros_like(r))
-        act = torch.nonzero(~free).reshape(-1)
         WtZr = dot(H.HS, 2 * R, [rF])[:, 0]
         if kk2:
+            act = torch.nonzero(~free).reshape(-1)  # a host sync: only where it is used
             rows_d = torch.as_tensor(rows, device=dev)
             GA = _gram(H.HS[rows_d[:, None], act[None, :]].double())
         else:
@@ -418,7 +418,7 @@ def _cauchy_point(dd, p0, M, theta, tc, nfin, g, HS, rows, fac, red, K):
             more = left > B
         found, tstar, c = _scan_batch(st, tb, gb, Wb, Mt, theta)
         if found:
-            return tstar, c.cpu().numpy()
+            return tstar, c
         ptr += mine_used
         B = min(B * 8, B_cap)
         if not more:
@@ -479,16 +479,22 @@ def _scan_batch(st, t, g, W, M, theta):
     fp_b = st["fp"] + torch.cumsum(dfp, 0) - dfp              # f' at the start of segment i
     dtmin = torch.where(fpp_b > 0, -fp_b / fpp_b, torch.full_like(fp_b, math.inf))
     stop = dtmin < dt
-    # one host copy: the first stop index (or -1) and the end-of-batch state
-    first = torch.where(stop.any(), torch.argmax(stop.to(torch.int8)).to(torch.float64),
+    # ONE host copy: the first stop index (or -1), the end-of-batch state, and -- formed on
+    # the device at that index, used only when it is >= 0 -- t* and c (three copies fewer
+    # per Cauchy point than reading t[j-1], dtmin[j] and c back one by one)
+    jt = torch.argmax(stop.to(torch.int8))
+    first = torch.where(stop.any(), jt.to(torch.float64),
                         torch.full((), -1.0, dtype=torch.float64, device=t.device))
-    tail = torch.stack([first, fp_b[-1] + dfp[-1], fpp_b[-1] + dfpp[-1], t[-1]]).cpu().numpy()
+    told_t = torch.where(jt > 0, t[(jt - 1).clamp(min=0)],
+                         torch.full((), told0, dtype=torch.float64, device=t.device))
+    dtm_t = dtmin[jt].clamp(min=0.0)
+    c_prev = torch.where(jt > 0, Cp[:, (jt - 1).clamp(min=0)], st["c"])
+    c_t = c_prev + dtm_t * P[:, jt]
+    tail = torch.cat([torch.stack([first, fp_b[-1] + dfp[-1], fpp_b[-1] + dfpp[-1], t[-1],
+                                   told_t + dtm_t]), c_t]).cpu().numpy()
     j = int(tail[0])
     if j >= 0:
-        told = told0 if j == 0 else float(t[j - 1].item())
-        dtm = max(float(dtmin[j].item()), 0.0)
-        c_prev = Cp[:, j - 1] if j > 0 else st["c"]
-        return True, told + dtm, c_prev + dtm * P[:, j]
+        return True, float(tail[4]), tail[5:]
     st["p"] = P[:, -1] + gw[:, -1]
     st["c"] = Cp[:, -1]
     st["fp"], st["fpp"], st["told"] = float(tail[1]), float(tail[2]), float(tail[3])
