@@ -2942,14 +2942,36 @@ struct EmLane7 {
   float inv, dw4, a1, a3, a5, a7;
 };
 
-__device__ __forceinline__ EmLane7 em_lane7(float inv, float delta) {
+// Fewer correction terms where the bin width allows (h is uniform for a shared sigma, so the
+// choice is one uniform branch per launch).  Maximum error of one halo's bin mass against
+// the exact Gaussian integral (float64 scan over the halo position, z in [-12, 12]):
+//   2 terms (B_2, B_4):       1.26e-7 at h = 0.35
+//   3 terms (+ B_6):          6.5e-8 at h = 0.5, 1.53e-7 at h = 0.55
+//   4 terms (+ B_8):          1.0e-8 at h = 0.55, 1.42e-7 at h = 0.7
+// all inside the per-edge tails' 1.6e-7 absolute contract.  The reference's GD benchmark
+// runs sigma from 0.5 to 0.2 at delta = 0.1 (h = 0.2 -> 0.5): 2 terms, then 3.  Each term
+// dropped saves one packed FMA per edge pair per halo.  MG_S2_ADAPTIVE=0: always 4 terms.
+#ifndef MG_S2_ADAPTIVE
+#define MG_S2_ADAPTIVE 1
+#endif
+constexpr float kS2H2 = 0.35f;    // 2 terms up to here
+constexpr float kS2H3 = 0.55f;    // 3 terms up to here, 4 terms up to kEmHMax2
+
+__device__ __forceinline__ int s2_em_terms(float h) {
+  if (!MG_S2_ADAPTIVE) return 4;
+  return h <= kS2H2 ? 2 : (h <= kS2H3 ? 3 : 4);
+}
+
+__device__ __forceinline__ EmLane7 em_lane7(float inv, float delta, int terms = 4) {
   constexpr float ik = 1.0f / kWScale;
   EmLane7 L;
   L.inv = inv;
   const float dw = delta * inv;
   L.dw4 = -4.0f * dw;
   const float h = dw * ik;
-  const float h2 = h * h, h4 = h2 * h2, h6 = h4 * h2, h8 = h4 * h4;
+  const float h2 = h * h, h4 = h2 * h2;
+  const float h6 = terms >= 3 ? h4 * h2 : 0.0f;
+  const float h8 = terms >= 4 ? h4 * h4 : 0.0f;
   const float ik2 = ik * ik;
   L.a1 = (h2 * (1.0f / 12.0f) + h4 * (3.0f / 720.0f) + h6 * (15.0f / 30240.0f) +
           h8 * (105.0f / 1209600.0f)) * ik;
@@ -3089,23 +3111,29 @@ __device__ __forceinline__ void smf2_accumulate(const float* __restrict__ x, int
   const int64_t step = (int64_t)kS2Ahead * stride;
   // EM range: uniform unpadded bins and h = delta / sigma <= kEmHMax2 (a uniform branch)
   if (b.delta > 0.0f && b.delta * isig <= kEmHMax2) {
-    const EmLane7 L = em_lane7(inv, b.delta);
+    const int terms = s2_em_terms(b.delta * isig);
+    const EmLane7 L = em_lane7(inv, b.delta, terms);
     const float nma = -a * inv;
     v2f E[EP::NV];
 #pragma unroll
     for (int i = 0; i < EP::NV; ++i) E[i] = (v2f)(0.0f);
-    float xa[kS2Ahead];
-    ld(first, xa);
-    for (int64_t w0 = first; w0 < n; w0 += step) {
-      float xb[kS2Ahead];
-      ld(w0 + step, xb);
+    auto em_loop = [&](auto a7c, auto a5c) {
+      float xa[kS2Ahead];
+      ld(first, xa);
+      for (int64_t w0 = first; w0 < n; w0 += step) {
+        float xb[kS2Ahead];
+        ld(w0 + step, xb);
 #pragma unroll
-      for (int u = 0; u < kS2Ahead; ++u) {
-        em_halo<NB, true, true>(fmaf(xa[u], -L.inv, nma), L.inv, L.dw4, L.a1, L.a3, L.a5, b, G, W,
-                                E, L.a7);
-        xa[u] = xb[u];
+        for (int u = 0; u < kS2Ahead; ++u) {
+          em_halo<NB, true, decltype(a7c)::value, decltype(a5c)::value>(
+              fmaf(xa[u], -L.inv, nma), L.inv, L.dw4, L.a1, L.a3, L.a5, b, G, W, E, L.a7);
+          xa[u] = xb[u];
+        }
       }
-    }
+    };
+    if (terms == 4) em_loop(std::true_type{}, std::true_type{});
+    else if (terms == 3) em_loop(std::false_type{}, std::true_type{});
+    else em_loop(std::false_type{}, std::false_type{});
     em2_finish<NB>(L, G, W, E, out);   // G, W become the residuals; the masses per bin
     return;
   } else {
@@ -3285,7 +3313,7 @@ __device__ __forceinline__ void vmem_wait_n() {  // s_waitcnt vmcnt(N), expcnt /
 // flight: the next tile lands while this one is evaluated), one ds_read per halo.  The lanes
 // forward of the population model stages its groups the same way; a register-prefetch loop
 // measured 400 us per 1e8 halos (4 waves / SIMD at 102 VGPRs: the loads were not covered).
-template <int NB>
+template <int NB, bool A7 = true, bool A5 = true>
 __device__ __forceinline__ void smf2_em_staged(const float* __restrict__ x, int64_t n,
                                                const EmLane7& L, float nma, const SmfBins& b,
                                                float* tiles, v2f (&G)[EdgePairs<NB>::NV],
@@ -3319,8 +3347,8 @@ __device__ __forceinline__ void smf2_em_staged(const float* __restrict__ x, int6
       const int64_t i = t * TH + r * kWave + lane;
       float xv = cur[r * kWave + lane];
       xv = i < n ? xv : kLaneSentinel;
-      em_halo<NB, true, true>(fmaf(xv, -L.inv, nma), L.inv, L.dw4, L.a1, L.a3, L.a5, b, G, W, E,
-                              L.a7);
+      em_halo<NB, true, A7, A5>(fmaf(xv, -L.inv, nma), L.inv, L.dw4, L.a1, L.a3, L.a5, b, G, W,
+                                E, L.a7);
     }
   }
 }
@@ -3345,12 +3373,15 @@ __global__ __launch_bounds__(kThreads, MG_S2_MINWAVES) void smf2_fwd_kernel(cons
   const float isig = inv_sigma<LOGSIG>(s);
   if (b.delta > 0.0f && b.delta * isig <= kEmHMax2) {
     const float inv = isig * kWScale;
-    const EmLane7 L = em_lane7(inv, b.delta);
+    const int terms = s2_em_terms(b.delta * isig);
+    const EmLane7 L = em_lane7(inv, b.delta, terms);
     v2f acc[EP::NV], G[EP::NV], W[EP::NV], E[EP::NV];
 #pragma unroll
     for (int i = 0; i < EP::NV; ++i) acc[i] = G[i] = W[i] = E[i] = (v2f)(0.0f);
-    smf2_em_staged<NB>(x, n, L, -a * inv, b, tiles + (threadIdx.x >> 6) * 2 * kS2Rows * kWave,
-                       G, W, E);
+    float* tw = tiles + (threadIdx.x >> 6) * 2 * kS2Rows * kWave;
+    if (terms == 4) smf2_em_staged<NB, true, true>(x, n, L, -a * inv, b, tw, G, W, E);
+    else if (terms == 3) smf2_em_staged<NB, false, true>(x, n, L, -a * inv, b, tw, G, W, E);
+    else smf2_em_staged<NB, false, false>(x, n, L, -a * inv, b, tw, G, W, E);
     em2_finish<NB>(L, G, W, E, v);
   } else {
     const int64_t first = (int64_t)blockIdx.x * kThreads + (threadIdx.x - lane);
