@@ -3294,9 +3294,11 @@ __device__ __attribute__((noinline)) S2Out<NB> smf2_edge_pass(const float* __res
   return o;
 }
 
-// Rows of 64 halos per LDS tile of the staged forward (two tiles per wave in flight).
+// Rows of 64 halos per LDS tile of the staged forward (two tiles per wave in flight).  16
+// measured best (profiles/r6_smf2/README.md, GD at 1e8 halos, same box: 3834-3847 it/s vs
+// 3746-3755 with 8 and 3586-3588 with 4; 32 KB of LDS per workgroup).
 #ifndef MG_S2_ROWS
-#define MG_S2_ROWS 8
+#define MG_S2_ROWS 16
 #endif
 constexpr int kS2Rows = MG_S2_ROWS;
 
